@@ -1,0 +1,157 @@
+/*
+ * storb_rs.h -- C ABI of the MI355X-native Storb Reed-Solomon path.
+ *
+ * This is the drop-in boundary for the chunk->shard erasure stage of
+ * crates/storb_base (reference @2025-08-01). Storb calls the external crate
+ * zfec-rs @3f3a3720 through exactly three entry points:
+ *
+ *   zfec_rs::Fec::new(k, m)           crates/storb_base/src/piece.rs:328,383
+ *   zfec_rs::Fec::encode(&[u8])       crates/storb_base/src/piece.rs:329
+ *   zfec_rs::Fec::decode(&Vec<Chunk>, padlen)
+ *                                     crates/storb_base/src/piece.rs:384-386
+ *   zfec_rs::Chunk::new(data, index)  crates/storb_base/src/piece.rs:375,378
+ *
+ * A zfec-rs-compatible Rust shim patched in through the
+ * workspace [patch] table maps those onto the functions below, so piece.rs,
+ * storb_validator and storb_miner compile unchanged. The storb sizing
+ * helpers (piece.rs:292-317) are exported too so every binding computes
+ * (k, m, B) identically.
+ *
+ * Notation: n = total share count = Storb's `m` (EncodedChunk.m, "Total
+ * blocks (data + parity)", piece.rs:190-191); n - k = parity shares. The
+ * headline "RS(k=4, m=2)" is k = 4, n = 6.
+ *
+ * Conventions: plain C types only; the caller owns every buffer; nothing
+ * here allocates or frees caller memory. Functions are thread-safe; a
+ * context serialises the calls made on it (use one context per thread for
+ * concurrency). Device pointers are HIP device memory of the context's GPU.
+ */
+#ifndef STORB_RS_H
+#define STORB_RS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes. zfec-rs returns Err(..) that the reference `.expect()`s
+ * (piece.rs:328-329,383-386): a shim maps any nonzero code to Err. */
+#define STORB_RS_OK 0
+#define STORB_RS_EINVAL 1     /* k < 1, k > n, n > 256, len == 0, bad index */
+#define STORB_RS_ENOTENOUGH 2 /* fewer than k distinct shares */
+#define STORB_RS_EDEVICE 3    /* HIP runtime failure (see storb_rs_last_error) */
+#define STORB_RS_ENOMEM 4     /* device or pinned allocation failed */
+#define STORB_RS_ENODEV 5     /* no usable gfx950 device */
+
+#define STORB_RS_MAX_SHARES 256 /* zfec: n <= 256 */
+
+typedef struct storb_rs_ctx storb_rs_ctx;
+
+/* ---- library / context --------------------------------------------- */
+const char *storb_rs_version(void);
+const char *storb_rs_strerror(int code);
+/* Number of HIP devices visible (0 when none; never an error). */
+int storb_rs_device_count(void);
+/* device_ordinal >= 0 pins the context to that GPU; -1 picks devices
+ * round-robin across contexts (objects partition across GPUs). */
+int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out);
+void storb_rs_ctx_destroy(storb_rs_ctx *ctx);
+int storb_rs_ctx_device(const storb_rs_ctx *ctx);
+/* Detail of the last failure on this context ("" if none). */
+const char *storb_rs_last_error(const storb_rs_ctx *ctx);
+
+/* ---- code parameters (host only, no GPU needed) ----------------------- */
+/* zfec-rs Fec::new validation: STORB_RS_OK or STORB_RS_EINVAL. */
+int storb_rs_check_params(uint32_t k, uint32_t n);
+/* The n*k systematic generator (rows 0..k-1 identity), row-major. */
+int storb_rs_enc_matrix(uint32_t k, uint32_t n, uint8_t *out_nk);
+/* Shard size zfec uses for a chunk of len bytes: ceil(len / k). */
+size_t storb_rs_block_size(uint32_t k, size_t len);
+/* piece.rs:292-303 piece_length(); min_size/max_size 0 = the constants
+ * of crates/storb_base/src/constants.rs:5-6 (16 KiB, 256 MiB). */
+uint64_t storb_piece_length(uint64_t content_length, uint64_t min_size,
+                            uint64_t max_size);
+/* piece.rs:307-317 get_k_and_m(): k data shares, m TOTAL shares. */
+void storb_get_k_and_m(uint64_t chunk_size, uint64_t *k, uint64_t *m);
+
+/* ---- host-in / host-out (zfec-rs Fec::encode / Fec::decode) ----------- */
+/* Encode one chunk: B = ceil(len/k), padlen = k*B - len. Writes the n-k
+ * parity shares (B bytes each) to parity_out[0..n-k). Data shares are the
+ * caller's own slices data[i*B, (i+1)*B) zero-padded (systematic code), so
+ * only parity crosses back. block_out / padlen_out may be NULL. */
+int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                    const uint8_t *data, size_t len,
+                    uint8_t *const *parity_out, size_t *block_out,
+                    size_t *padlen_out);
+/* Decode one chunk from nshares >= k shares (any order). Selection follows
+ * decode_chunk (piece.rs:368-381): sort by index, keep the first k. Writes
+ * k*block - padlen bytes to out. */
+int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                    const uint8_t *const *shares, const uint32_t *share_idx,
+                    uint32_t nshares, size_t block, size_t padlen,
+                    uint8_t *out);
+
+/* Pipelined host batch: nchunks equal-length chunks laid out back to back
+ * in host memory (chunk c at data + c*chunk_len). Parity of chunk c, share
+ * p lands at parity_out + (c*(n-k) + p)*B. Uses pinned staging and
+ * overlapped H2D / kernel / D2H on the context's streams. */
+int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                           const uint8_t *data, size_t chunk_len,
+                           uint32_t nchunks, uint8_t *parity_out);
+
+/* ---- device-resident batched variants -------------------------------- */
+/* Stripe s, data share j lives at d_data + s*data_stride + j*block; parity
+ * share p at d_parity + s*parity_stride + p*block. Strides of 0 mean the
+ * packed defaults k*block and (n-k)*block. Asynchronous on `hip_stream`
+ * (a hipStream_t; NULL = the context's own stream). */
+int storb_rs_encode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                              size_t block, uint32_t nstripes,
+                              const uint8_t *d_data, size_t data_stride,
+                              uint8_t *d_parity, size_t parity_stride,
+                              void *hip_stream);
+/* Reconstruct the data shares of nstripes stripes that all lost the same
+ * shares. share_idx lists the nshares >= k surviving share indices (first k
+ * by index are used). Survivor i < k is read from the data region, i >= k
+ * from the parity region. Only the missing data rows are computed (zfec).
+ * They are written into d_out (same layout as d_data, stride out_stride);
+ * when d_out != d_data the surviving data shares are copied there as well,
+ * when d_out == d_data the reconstruction is in place. */
+int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                              size_t block, uint32_t nstripes,
+                              const uint32_t *share_idx, uint32_t nshares,
+                              const uint8_t *d_data, size_t data_stride,
+                              const uint8_t *d_parity, size_t parity_stride,
+                              uint8_t *d_out, size_t out_stride,
+                              void *hip_stream);
+/* The primitive under both: out_r = XOR_j coef[r*k + j] * in_j over GF(2^8)
+ * for r < rows, for every stripe (shard s of slot j at d_in[j] +
+ * s*in_stride[j]). Serves repair (regenerate any share row). */
+int storb_rs_apply_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t rows,
+                       const uint8_t *coef, const uint8_t *const *d_in,
+                       const size_t *in_stride, uint8_t *const *d_out,
+                       const size_t *out_stride, size_t block,
+                       uint32_t nstripes, void *hip_stream);
+
+/* ---- synthetic input (benchmarks / tests) ----------------------------- */
+/* Object o (o < nobj) at d + o*obj_stride gets obj_len bytes of the
+ * little-endian splitmix64 stream seeded with seed_base + o. */
+int storb_rs_fill_splitmix_dev(storb_rs_ctx *ctx, uint8_t *d, size_t obj_len,
+                               uint32_t nobj, size_t obj_stride,
+                               uint64_t seed_base, void *hip_stream);
+
+/* Which kernel variant the dev calls launch (0 = auto). Benchmarks use it
+ * to time the LDS-table variant beside the register-table one. */
+#define STORB_RS_KERNEL_AUTO 0
+#define STORB_RS_KERNEL_PERM 1 /* nibble tables in registers, v_perm_b32 */
+#define STORB_RS_KERNEL_LDS 2  /* 256-B product tables staged in LDS */
+int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant);
+
+/* Synchronise the context's stream(s). */
+int storb_rs_sync(storb_rs_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STORB_RS_H */

@@ -1,0 +1,270 @@
+"""ctypes binding of the C ABI in include/storb_rs.h (libstorb_rs.so).
+
+There is no fallback: if the HIP library is missing, importing this module
+raises. Host-only entry points (sizing, generator matrix, parameter checks)
+work without a GPU; every compute entry point needs a gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libstorb_rs.so")
+
+OK, EINVAL, ENOTENOUGH, EDEVICE, ENOMEM, ENODEV = range(6)
+KERNEL_AUTO, KERNEL_PERM, KERNEL_LDS = 0, 1, 2
+
+
+class StorbRsError(RuntimeError):
+    def __init__(self, code: int, detail: str = ""):
+        self.code = code
+        msg = lib().storb_rs_strerror(code).decode()
+        super().__init__(f"{msg}{': ' + detail if detail else ''} (code {code})")
+
+
+def build(jobs: int = 8) -> str:
+    """Compile the HIP library in-tree for gfx950 (make -C storb_amd)."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", PKG_DIR], check=True)
+    return LIB_PATH
+
+
+_lib = None
+_lock = threading.Lock()
+
+u8p = C.POINTER(C.c_uint8)
+vp = C.c_void_p
+sz = C.c_size_t
+
+
+def _declare(L):
+    L.storb_rs_version.restype = C.c_char_p
+    L.storb_rs_strerror.restype = C.c_char_p
+    L.storb_rs_strerror.argtypes = [C.c_int]
+    L.storb_rs_device_count.restype = C.c_int
+    L.storb_rs_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.storb_rs_ctx_destroy.argtypes = [vp]
+    L.storb_rs_ctx_destroy.restype = None
+    L.storb_rs_ctx_device.argtypes = [vp]
+    L.storb_rs_last_error.argtypes = [vp]
+    L.storb_rs_last_error.restype = C.c_char_p
+    L.storb_rs_check_params.argtypes = [C.c_uint32, C.c_uint32]
+    L.storb_rs_enc_matrix.argtypes = [C.c_uint32, C.c_uint32, vp]
+    L.storb_rs_block_size.argtypes = [C.c_uint32, sz]
+    L.storb_rs_block_size.restype = sz
+    L.storb_piece_length.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+    L.storb_piece_length.restype = C.c_uint64
+    L.storb_get_k_and_m.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.storb_get_k_and_m.restype = None
+    L.storb_rs_encode.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.POINTER(vp),
+                                  C.POINTER(sz), C.POINTER(sz)]
+    L.storb_rs_decode.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(vp),
+                                  C.POINTER(C.c_uint32), C.c_uint32, sz, sz, vp]
+    L.storb_rs_encode_chunks.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.c_uint32, vp]
+    L.storb_rs_encode_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
+                                            vp, sz, vp, sz, vp]
+    L.storb_rs_decode_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
+                                            C.POINTER(C.c_uint32), C.c_uint32, vp, sz, vp,
+                                            sz, vp, sz, vp]
+    L.storb_rs_apply_dev.argtypes = [vp, C.c_uint32, C.c_uint32, vp, C.POINTER(vp),
+                                     C.POINTER(sz), C.POINTER(vp), C.POINTER(sz), sz,
+                                     C.c_uint32, vp]
+    L.storb_rs_fill_splitmix_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, C.c_uint64, vp]
+    L.storb_rs_set_kernel.argtypes = [vp, C.c_int]
+    L.storb_rs_sync.argtypes = [vp]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(
+                        f"{LIB_PATH} is missing: the MI355X library must be built "
+                        "(python -c 'import __graft_entry__ as g; g.build()'); there is "
+                        "no CPU fallback")
+                L = C.CDLL(LIB_PATH)
+                _declare(L)
+                _lib = L
+    return _lib
+
+
+# ------------------------------------------------------------ host-only
+def version() -> str:
+    return lib().storb_rs_version().decode()
+
+
+def device_count() -> int:
+    return int(lib().storb_rs_device_count())
+
+
+def check_params(k: int, n: int) -> bool:
+    if not (0 <= k < 2**32 and 0 <= n < 2**32):
+        return False
+    return lib().storb_rs_check_params(k, n) == OK
+
+
+def enc_matrix(k: int, n: int) -> np.ndarray:
+    out = np.zeros(n * k, dtype=np.uint8)
+    rc = lib().storb_rs_enc_matrix(k, n, out.ctypes.data)
+    if rc != OK:
+        raise StorbRsError(rc, f"(k={k}, n={n})")
+    return out.reshape(n, k)
+
+
+def block_size(k: int, length: int) -> int:
+    return int(lib().storb_rs_block_size(k, length))
+
+
+def piece_length(content_length: int, min_size: int = 0, max_size: int = 0) -> int:
+    return int(lib().storb_piece_length(content_length, min_size, max_size))
+
+
+def get_k_and_m(chunk_size: int) -> tuple[int, int]:
+    k, m = C.c_uint64(), C.c_uint64()
+    lib().storb_get_k_and_m(chunk_size, C.byref(k), C.byref(m))
+    return int(k.value), int(m.value)
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+class Context:
+    """One storb_rs_ctx: a GPU, its streams, staging and table caches."""
+
+    def __init__(self, device: int = -1):
+        h = vp()
+        rc = lib().storb_rs_ctx_create(device, C.byref(h))
+        if rc != OK:
+            raise StorbRsError(rc, "storb_rs_ctx_create")
+        self._h = h
+        # hipStream_t used when a call passes stream=None (None -> the
+        # context's own stream). Tests point it at torch's current stream.
+        self.default_stream: Optional[int] = None
+
+    def _s(self, stream):
+        return self.default_stream if stream is None else stream
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def device(self) -> int:
+        return int(lib().storb_rs_ctx_device(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().storb_rs_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != OK:
+            detail = lib().storb_rs_last_error(self._h).decode()
+            raise StorbRsError(rc, f"{what}: {detail}" if detail else what)
+
+    # ---------------------------------------------------- host buffers
+    def encode(self, k: int, n: int, data) -> tuple[list[bytes], int, int]:
+        buf = _as_u8(data)
+        B = block_size(k, buf.size) if k else 0
+        p = max(n - k, 0)
+        outs = [np.zeros(max(B, 1), dtype=np.uint8) for _ in range(p)]
+        ptrs = (vp * max(p, 1))(*[o.ctypes.data for o in outs])
+        b, pad = sz(), sz()
+        rc = lib().storb_rs_encode(self._h, k, n, buf.ctypes.data if buf.size else None,
+                                   buf.size, ptrs, C.byref(b), C.byref(pad))
+        self._check(rc, "storb_rs_encode")
+        return [o[: b.value].tobytes() for o in outs], int(b.value), int(pad.value)
+
+    def decode(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
+               padlen: int) -> bytes:
+        arrs = [_as_u8(s) for s in shares]
+        ptrs = (vp * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
+        ids = (C.c_uint32 * max(len(idx), 1))(*idx)
+        outlen = max(k * block - padlen, 0)
+        out = np.zeros(max(outlen, 1), dtype=np.uint8)
+        rc = lib().storb_rs_decode(self._h, k, n, ptrs, ids, len(arrs), block, padlen,
+                                   out.ctypes.data)
+        self._check(rc, "storb_rs_decode")
+        return out[:outlen].tobytes()
+
+    def encode_chunks(self, k: int, n: int, data: np.ndarray, chunk_len: int,
+                      nchunks: int) -> np.ndarray:
+        buf = _as_u8(data)
+        assert buf.size >= chunk_len * nchunks
+        B = block_size(k, chunk_len)
+        out = np.empty(nchunks * (n - k) * B, dtype=np.uint8)
+        rc = lib().storb_rs_encode_chunks(self._h, k, n, buf.ctypes.data, chunk_len,
+                                          nchunks, out.ctypes.data)
+        self._check(rc, "storb_rs_encode_chunks")
+        return out
+
+    # --------------------------------------------------- device buffers
+    def encode_batch_dev(self, k: int, n: int, block: int, nstripes: int, d_data: int,
+                         d_parity: int, data_stride: int = 0, parity_stride: int = 0,
+                         stream: Optional[int] = None):
+        rc = lib().storb_rs_encode_batch_dev(self._h, k, n, block, nstripes, d_data,
+                                             data_stride, d_parity, parity_stride, self._s(stream))
+        self._check(rc, "storb_rs_encode_batch_dev")
+
+    def decode_batch_dev(self, k: int, n: int, block: int, nstripes: int,
+                         share_idx: Sequence[int], d_data: int, d_parity: int, d_out: int,
+                         data_stride: int = 0, parity_stride: int = 0, out_stride: int = 0,
+                         stream: Optional[int] = None):
+        ids = (C.c_uint32 * max(len(share_idx), 1))(*share_idx)
+        rc = lib().storb_rs_decode_batch_dev(self._h, k, n, block, nstripes, ids,
+                                             len(share_idx), d_data, data_stride, d_parity,
+                                             parity_stride, d_out, out_stride, self._s(stream))
+        self._check(rc, "storb_rs_decode_batch_dev")
+
+    def apply_dev(self, coef: np.ndarray, d_in: Sequence[int], in_stride: Sequence[int],
+                  d_out: Sequence[int], out_stride: Sequence[int], block: int,
+                  nstripes: int, stream: Optional[int] = None):
+        coef = np.ascontiguousarray(coef, dtype=np.uint8)
+        rows, k = coef.shape
+        ins = (vp * k)(*d_in)
+        inst = (sz * k)(*in_stride)
+        outs = (vp * rows)(*d_out)
+        outst = (sz * rows)(*out_stride)
+        rc = lib().storb_rs_apply_dev(self._h, k, rows, coef.ctypes.data, ins, inst, outs,
+                                      outst, block, nstripes, self._s(stream))
+        self._check(rc, "storb_rs_apply_dev")
+
+    def fill_splitmix_dev(self, d: int, obj_len: int, nobj: int, obj_stride: int = 0,
+                          seed_base: int = 0, stream: Optional[int] = None):
+        rc = lib().storb_rs_fill_splitmix_dev(self._h, d, obj_len, nobj, obj_stride,
+                                              seed_base, self._s(stream))
+        self._check(rc, "storb_rs_fill_splitmix_dev")
+
+    def set_kernel(self, variant: int):
+        self._check(lib().storb_rs_set_kernel(self._h, variant), "storb_rs_set_kernel")
+
+    def sync(self):
+        self._check(lib().storb_rs_sync(self._h), "storb_rs_sync")
+
+
+_tls = threading.local()
+
+
+def thread_context() -> Context:
+    """Per-thread context (the Rust shim's OnceLock analogue)."""
+    ctx = getattr(_tls, "ctx", None)
+    if ctx is None:
+        ctx = Context(-1)
+        _tls.ctx = ctx
+    return ctx

@@ -1,0 +1,702 @@
+// storb_rs.cpp -- implementation of the C ABI in include/storb_rs.h.
+//
+// Host side of the MI355X Reed-Solomon path: parameter checks and generator
+// matrices (mirroring zfec-rs Fec::new, reached from piece.rs:328,383),
+// decode-matrix construction (Fec::decode, piece.rs:384-386), coefficient
+// table caches, pinned staging, streams, and the tiling of arbitrary
+// (rows x k) matrices onto the 16 x 32 slot kernels of rs_kernels.hip.
+#include "../../include/storb_rs.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gf256.hpp"
+#include "rs_kernels.hpp"
+
+using namespace storb_rs;
+
+namespace {
+
+constexpr size_t kAlign = 16;
+inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct DevBuf {
+  uint8_t *p = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), n);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+};
+
+struct PinBuf {
+  uint8_t *p = nullptr;
+  size_t cap = 0;
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+};
+
+// Device-resident coefficient tables for one (rows x k) matrix, tiled in
+// kSlotR x kSlotK blocks: for block b, ptab + b_off[b] PermTabs and
+// btab + b_off[b]*256 product-table bytes.
+struct Tables {
+  uint8_t *dev = nullptr;
+  size_t perm_bytes = 0;
+  std::vector<size_t> b_off;
+  ~Tables() {
+    if (dev) (void)hipFree(dev);
+  }
+};
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+std::mutex g_enc_mu;
+std::map<std::pair<uint32_t, uint32_t>, std::vector<uint8_t>> g_enc;
+
+const std::vector<uint8_t> &cached_enc(uint32_t k, uint32_t n) {
+  std::lock_guard<std::mutex> lk(g_enc_mu);
+  auto key = std::make_pair(k, n);
+  auto it = g_enc.find(key);
+  if (it == g_enc.end()) it = g_enc.emplace(key, enc_matrix(k, n)).first;
+  return it->second;
+}
+
+std::atomic<int> g_rr{0};
+
+}  // namespace
+
+struct storb_rs_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t pipe[2] = {nullptr, nullptr};
+  int variant = STORB_RS_KERNEL_AUTO;
+  std::mutex mu;
+  std::string last_error;
+  DevBuf stage;
+  DevBuf pipe_dev[2];
+  PinBuf pin_in, pin_out;
+  PinBuf pipe_in[2], pipe_out[2];
+  std::map<std::vector<uint8_t>, std::unique_ptr<Tables>> tables;
+};
+
+namespace {
+
+int fail(storb_rs_ctx *ctx, int code, const std::string &msg) {
+  if (ctx) ctx->last_error = msg;
+  return code;
+}
+
+int hip_fail(storb_rs_ctx *ctx, hipError_t e, const char *what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(ctx, e == hipErrorOutOfMemory ? STORB_RS_ENOMEM : STORB_RS_EDEVICE, m);
+}
+
+#define HIP_TRY(ctx, expr)                              \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+  } while (0)
+
+Variant pick_variant(const storb_rs_ctx *ctx) {
+  return ctx->variant == STORB_RS_KERNEL_LDS ? Variant::Lds : Variant::Perm;
+}
+
+// Build (or fetch) the device tables of a rows x k coefficient matrix.
+int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
+               hipStream_t s, const Tables **out) {
+  std::vector<uint8_t> key(8 + static_cast<size_t>(rows) * k);
+  std::memcpy(key.data(), &k, 4);
+  std::memcpy(key.data() + 4, &rows, 4);
+  std::memcpy(key.data() + 8, coef, static_cast<size_t>(rows) * k);
+  auto it = ctx->tables.find(key);
+  if (it != ctx->tables.end()) {
+    *out = it->second.get();
+    return STORB_RS_OK;
+  }
+  if (ctx->tables.size() > 4096) ctx->tables.clear();
+  auto t = std::make_unique<Tables>();
+  // Count coefficients per block in the same order the launcher walks.
+  size_t total = 0;
+  for (uint32_t rb = 0; rb < rows; rb += kSlotR)
+    for (uint32_t cb = 0; cb < k; cb += kSlotK) {
+      t->b_off.push_back(total);
+      total += static_cast<size_t>(std::min<uint32_t>(kSlotR, rows - rb)) *
+               std::min<uint32_t>(kSlotK, k - cb);
+    }
+  t->perm_bytes = round_up(total * sizeof(PermTab), 256);
+  std::vector<uint8_t> host(t->perm_bytes + total * 256, 0);
+  PermTab *pt = reinterpret_cast<PermTab *>(host.data());
+  uint8_t *bt = host.data() + t->perm_bytes;
+  const GF256 &g = gf();
+  size_t bi = 0;
+  for (uint32_t rb = 0; rb < rows; rb += kSlotR)
+    for (uint32_t cb = 0; cb < k; cb += kSlotK, bi++) {
+      const uint32_t rr = std::min<uint32_t>(kSlotR, rows - rb);
+      const uint32_t kk = std::min<uint32_t>(kSlotK, k - cb);
+      for (uint32_t i = 0; i < rr; i++)
+        for (uint32_t j = 0; j < kk; j++) {
+          const uint8_t c = coef[static_cast<size_t>(rb + i) * k + cb + j];
+          const size_t o = t->b_off[bi] + static_cast<size_t>(i) * kk + j;
+          pt[o] = perm_tab(c);
+          for (int x = 0; x < 256; x++) bt[o * 256 + x] = g.mul(c, static_cast<uint8_t>(x));
+        }
+    }
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&t->dev), host.size());
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tables)");
+  e = hipMemcpyAsync(t->dev, host.data(), host.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "upload tables");
+  *out = t.get();
+  ctx->tables.emplace(std::move(key), std::move(t));
+  return STORB_RS_OK;
+}
+
+// out_r = sum_j coef[r][j] * in_j for all stripes, tiled into slot blocks.
+int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
+          const uint8_t *const *d_in, const size_t *in_stride, uint8_t *const *d_out,
+          const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s) {
+  if (rows == 0 || block == 0 || nstripes == 0) return STORB_RS_OK;
+  const Tables *t = nullptr;
+  int rc = get_tables(ctx, k, rows, coef, s, &t);
+  if (rc) return rc;
+  const Variant v = pick_variant(ctx);
+  size_t bi = 0;
+  for (uint32_t rb = 0; rb < rows; rb += kSlotR)
+    for (uint32_t cb = 0; cb < k; cb += kSlotK, bi++) {
+      ApplyArgs a{};
+      a.r = std::min<uint32_t>(kSlotR, rows - rb);
+      a.k = std::min<uint32_t>(kSlotK, k - cb);
+      for (uint32_t j = 0; j < a.k; j++) {
+        a.in[j] = d_in[cb + j];
+        a.in_stride[j] = in_stride[cb + j];
+      }
+      for (uint32_t i = 0; i < a.r; i++) {
+        a.out[i] = d_out[rb + i];
+        a.out_stride[i] = out_stride[rb + i];
+      }
+      a.ptab = reinterpret_cast<const PermTab *>(t->dev) + t->b_off[bi];
+      a.btab = t->dev + t->perm_bytes + t->b_off[bi] * 256;
+      a.block = block;
+      a.nstripes = nstripes;
+      a.accumulate = cb > 0 ? 1 : 0;
+      HIP_TRY(ctx, launch_apply(a, v, s));
+    }
+  return STORB_RS_OK;
+}
+
+// decode_chunk selection (piece.rs:368-381): sort by index, keep first k,
+// then zfec's slot arrangement: primary share s in slot s, parity shares
+// fill the holes in index order. Returns the k slot share-indices and the
+// position in share_idx[] of each.
+int select_shares(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint32_t *share_idx,
+                  uint32_t nshares, std::vector<uint32_t> &slot_idx,
+                  std::vector<uint32_t> &slot_pos) {
+  if (nshares < k)
+    return fail(ctx, STORB_RS_ENOTENOUGH, "fewer than k shares supplied");
+  std::vector<uint32_t> ord(nshares);
+  for (uint32_t i = 0; i < nshares; i++) {
+    if (share_idx[i] >= n) return fail(ctx, STORB_RS_EINVAL, "share index >= n");
+    ord[i] = i;
+  }
+  std::stable_sort(ord.begin(), ord.end(),
+                   [&](uint32_t a, uint32_t b) { return share_idx[a] < share_idx[b]; });
+  ord.resize(k);
+  for (uint32_t i = 1; i < k; i++)
+    if (share_idx[ord[i]] == share_idx[ord[i - 1]])
+      return fail(ctx, STORB_RS_ENOTENOUGH, "duplicate share index among the first k");
+  slot_idx.assign(k, UINT32_MAX);
+  slot_pos.assign(k, UINT32_MAX);
+  for (uint32_t i = 0; i < k; i++) {
+    const uint32_t id = share_idx[ord[i]];
+    if (id < k) {
+      slot_idx[id] = id;
+      slot_pos[id] = ord[i];
+    }
+  }
+  uint32_t s = 0;
+  for (uint32_t i = 0; i < k; i++) {
+    const uint32_t id = share_idx[ord[i]];
+    if (id < k) continue;
+    while (slot_idx[s] != UINT32_MAX) s++;
+    slot_idx[s] = id;
+    slot_pos[s] = ord[i];
+  }
+  return STORB_RS_OK;
+}
+
+// Rows of D^-1 that rebuild the missing data shares. missing[r] = the data
+// index (= slot) of output row r.
+int decode_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                const std::vector<uint32_t> &slot_idx, std::vector<uint8_t> &coef,
+                std::vector<uint32_t> &missing) {
+  missing.clear();
+  for (uint32_t s = 0; s < k; s++)
+    if (slot_idx[s] >= k) missing.push_back(s);
+  if (missing.empty()) return STORB_RS_OK;
+  const std::vector<uint8_t> &enc = cached_enc(k, n);
+  std::vector<uint8_t> d(static_cast<size_t>(k) * k, 0);
+  for (uint32_t s = 0; s < k; s++)
+    std::memcpy(&d[static_cast<size_t>(s) * k], &enc[static_cast<size_t>(slot_idx[s]) * k], k);
+  if (!gf_invert(d, k)) return fail(ctx, STORB_RS_EINVAL, "singular decode matrix");
+  coef.resize(missing.size() * k);
+  for (size_t r = 0; r < missing.size(); r++)
+    std::memcpy(&coef[r * k], &d[static_cast<size_t>(missing[r]) * k], k);
+  return STORB_RS_OK;
+}
+
+hipStream_t pick_stream(storb_rs_ctx *ctx, void *s) {
+  return s ? reinterpret_cast<hipStream_t>(s) : ctx->stream;
+}
+
+}  // namespace
+
+// ======================================================================
+extern "C" {
+
+const char *storb_rs_version(void) { return "storb-rs-mi355x 0.1.0 (gfx950)"; }
+
+const char *storb_rs_strerror(int code) {
+  switch (code) {
+    case STORB_RS_OK: return "ok";
+    case STORB_RS_EINVAL: return "invalid argument";
+    case STORB_RS_ENOTENOUGH: return "not enough distinct shares to decode";
+    case STORB_RS_EDEVICE: return "HIP device error";
+    case STORB_RS_ENOMEM: return "out of memory";
+    case STORB_RS_ENODEV: return "no usable gfx950 device";
+    default: return "unknown error";
+  }
+}
+
+int storb_rs_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
+  if (!out) return STORB_RS_EINVAL;
+  *out = nullptr;
+  const int ndev = storb_rs_device_count();
+  if (ndev <= 0) return STORB_RS_ENODEV;
+  int dev = device_ordinal;
+  if (dev < 0) dev = g_rr.fetch_add(1) % ndev;
+  if (dev >= ndev) return STORB_RS_EINVAL;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return STORB_RS_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return STORB_RS_ENODEV;
+  DeviceGuard g(dev);
+  if (!g.ok) return STORB_RS_ENODEV;
+  auto *c = new storb_rs_ctx();
+  c->device = dev;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) != hipSuccess) {
+    storb_rs_ctx_destroy(c);
+    return STORB_RS_EDEVICE;
+  }
+  *out = c;
+  return STORB_RS_OK;
+}
+
+void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
+  if (!ctx) return;
+  DeviceGuard g(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto &p : ctx->pipe)
+    if (p) (void)hipStreamSynchronize(p);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  for (auto &p : ctx->pipe)
+    if (p) (void)hipStreamDestroy(p);
+  delete ctx;  // frees tables, staging and pinned buffers on ctx->device
+}
+
+int storb_rs_ctx_device(const storb_rs_ctx *ctx) { return ctx ? ctx->device : -1; }
+
+const char *storb_rs_last_error(const storb_rs_ctx *ctx) {
+  return ctx ? ctx->last_error.c_str() : "";
+}
+
+int storb_rs_check_params(uint32_t k, uint32_t n) {
+  return valid_params(k, n) ? STORB_RS_OK : STORB_RS_EINVAL;
+}
+
+int storb_rs_enc_matrix(uint32_t k, uint32_t n, uint8_t *out_nk) {
+  if (!valid_params(k, n) || !out_nk) return STORB_RS_EINVAL;
+  const std::vector<uint8_t> &e = cached_enc(k, n);
+  std::memcpy(out_nk, e.data(), e.size());
+  return STORB_RS_OK;
+}
+
+size_t storb_rs_block_size(uint32_t k, size_t len) {
+  return k ? (len + k - 1) / k : 0;
+}
+
+// piece.rs:292-303. `f64 as i32` saturates (NaN -> 0, -inf -> i32::MIN);
+// release-mode `1u64 << e` masks the shift to e & 63.
+uint64_t storb_piece_length(uint64_t content_length, uint64_t min_size,
+                            uint64_t max_size) {
+  if (min_size == 0) min_size = 16ull * 1024;           // constants.rs:5
+  if (max_size == 0) max_size = 256ull * 1024 * 1024;   // constants.rs:6
+  const double e = std::log2(static_cast<double>(content_length)) * 0.5 + 8.39;
+  int32_t ei;
+  if (std::isnan(e)) ei = 0;
+  else if (e <= -2147483648.0) ei = INT32_MIN;
+  else if (e >= 2147483647.0) ei = INT32_MAX;
+  else ei = static_cast<int32_t>(e);
+  uint64_t len = 1ull << (static_cast<uint32_t>(ei) & 63u);
+  return std::min(std::max(len, min_size), max_size);
+}
+
+void storb_get_k_and_m(uint64_t chunk_size, uint64_t *k, uint64_t *m) {
+  const uint64_t ps = storb_piece_length(chunk_size, 0, 0);
+  const uint64_t kk = static_cast<uint64_t>(
+      std::ceil(static_cast<double>(chunk_size) / static_cast<double>(ps)));
+  const uint64_t pp = static_cast<uint64_t>(std::ceil(static_cast<double>(kk) / 2.0));
+  if (k) *k = kk;
+  if (m) *m = kk + pp;
+}
+
+int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant) {
+  if (!ctx || variant < 0 || variant > 2) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->variant = variant;
+  return STORB_RS_OK;
+}
+
+int storb_rs_sync(storb_rs_ctx *ctx) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard g(ctx->device);
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (auto &p : ctx->pipe) HIP_TRY(ctx, hipStreamSynchronize(p));
+  return STORB_RS_OK;
+}
+
+// ---------------------------------------------------------------- device
+int storb_rs_apply_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
+                       const uint8_t *const *d_in, const size_t *in_stride,
+                       uint8_t *const *d_out, const size_t *out_stride, size_t block,
+                       uint32_t nstripes, void *hip_stream) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (k < 1 || k > STORB_RS_MAX_SHARES || rows > STORB_RS_MAX_SHARES || !coef ||
+      !d_in || !in_stride || !d_out || !out_stride)
+    return fail(ctx, STORB_RS_EINVAL, "apply: bad arguments");
+  DeviceGuard g(ctx->device);
+  return apply(ctx, k, rows, coef, d_in, in_stride, d_out, out_stride, block, nstripes,
+               pick_stream(ctx, hip_stream));
+}
+
+int storb_rs_encode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                              uint32_t nstripes, const uint8_t *d_data,
+                              size_t data_stride, uint8_t *d_parity,
+                              size_t parity_stride, void *hip_stream) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (n == k || block == 0 || nstripes == 0) return STORB_RS_OK;
+  if (!d_data || !d_parity) return fail(ctx, STORB_RS_EINVAL, "null device pointer");
+  if (data_stride == 0) data_stride = static_cast<size_t>(k) * block;
+  if (parity_stride == 0) parity_stride = static_cast<size_t>(n - k) * block;
+  DeviceGuard g(ctx->device);
+  const std::vector<uint8_t> &enc = cached_enc(k, n);
+  const uint32_t p = n - k;
+  std::vector<const uint8_t *> in(k);
+  std::vector<size_t> ins(k, data_stride), outs(p, parity_stride);
+  std::vector<uint8_t *> out(p);
+  for (uint32_t j = 0; j < k; j++) in[j] = d_data + static_cast<size_t>(j) * block;
+  for (uint32_t i = 0; i < p; i++) out[i] = d_parity + static_cast<size_t>(i) * block;
+  return apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(), ins.data(),
+               out.data(), outs.data(), block, nstripes, pick_stream(ctx, hip_stream));
+}
+
+int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                              uint32_t nstripes, const uint32_t *share_idx,
+                              uint32_t nshares, const uint8_t *d_data,
+                              size_t data_stride, const uint8_t *d_parity,
+                              size_t parity_stride, uint8_t *d_out, size_t out_stride,
+                              void *hip_stream) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (!share_idx || !d_out) return fail(ctx, STORB_RS_EINVAL, "null argument");
+  if (data_stride == 0) data_stride = static_cast<size_t>(k) * block;
+  if (parity_stride == 0) parity_stride = static_cast<size_t>(n - k) * block;
+  if (out_stride == 0) out_stride = static_cast<size_t>(k) * block;
+  std::vector<uint32_t> slot_idx, slot_pos, missing;
+  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint8_t> coef;
+  rc = decode_rows(ctx, k, n, slot_idx, coef, missing);
+  if (rc) return rc;
+  if (block == 0 || nstripes == 0) return STORB_RS_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = pick_stream(ctx, hip_stream);
+  std::vector<const uint8_t *> in(k);
+  std::vector<size_t> ins(k);
+  for (uint32_t c = 0; c < k; c++) {
+    const uint32_t id = slot_idx[c];
+    if (id < k) {
+      if (!d_data) return fail(ctx, STORB_RS_EINVAL, "survivor in null data region");
+      in[c] = d_data + static_cast<size_t>(id) * block;
+      ins[c] = data_stride;
+    } else {
+      if (!d_parity) return fail(ctx, STORB_RS_EINVAL, "survivor in null parity region");
+      in[c] = d_parity + static_cast<size_t>(id - k) * block;
+      ins[c] = parity_stride;
+    }
+  }
+  // Surviving data shares: in place when d_out aliases d_data, else copied.
+  if (d_out != d_data || out_stride != data_stride) {
+    for (uint32_t c = 0; c < k; c++)
+      if (slot_idx[c] < k)
+        HIP_TRY(ctx, hipMemcpy2DAsync(d_out + static_cast<size_t>(c) * block, out_stride,
+                                      in[c], ins[c], block, nstripes,
+                                      hipMemcpyDeviceToDevice, s));
+  }
+  if (missing.empty()) return STORB_RS_OK;
+  std::vector<uint8_t *> out(missing.size());
+  std::vector<size_t> outs(missing.size(), out_stride);
+  for (size_t r = 0; r < missing.size(); r++)
+    out[r] = d_out + static_cast<size_t>(missing[r]) * block;
+  return apply(ctx, k, static_cast<uint32_t>(missing.size()), coef.data(), in.data(),
+               ins.data(), out.data(), outs.data(), block, nstripes, s);
+}
+
+int storb_rs_fill_splitmix_dev(storb_rs_ctx *ctx, uint8_t *d, size_t obj_len,
+                               uint32_t nobj, size_t obj_stride, uint64_t seed_base,
+                               void *hip_stream) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!d && obj_len && nobj) return fail(ctx, STORB_RS_EINVAL, "null device pointer");
+  if (obj_stride == 0) obj_stride = obj_len;
+  DeviceGuard g(ctx->device);
+  HIP_TRY(ctx, launch_fill_splitmix(d, obj_len, nobj, obj_stride, seed_base,
+                                    pick_stream(ctx, hip_stream)));
+  return STORB_RS_OK;
+}
+
+// ------------------------------------------------------------------ host
+int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                    size_t len, uint8_t *const *parity_out, size_t *block_out,
+                    size_t *padlen_out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
+  const size_t B = (len + k - 1) / k, pad = B * k - len;
+  if (block_out) *block_out = B;
+  if (padlen_out) *padlen_out = pad;
+  const uint32_t p = n - k;
+  if (p == 0) return STORB_RS_OK;
+  if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  const size_t S = round_up(B, kAlign);
+  DeviceGuard g(ctx->device);
+  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(p) * S));
+  HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(n) * S));
+  // Zero-padded data shares, S-pitched (zfec pads the tail with zeros).
+  uint8_t *hin = ctx->pin_in.p;
+  for (uint32_t j = 0; j < k; j++) {
+    const size_t off = static_cast<size_t>(j) * B;
+    const size_t cnt = off < len ? std::min(B, len - off) : 0;
+    if (cnt) std::memcpy(hin + static_cast<size_t>(j) * S, data + off, cnt);
+    std::memset(hin + static_cast<size_t>(j) * S + cnt, 0, S - cnt);
+  }
+  hipStream_t s = ctx->stream;
+  uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
+  HIP_TRY(ctx, hipMemcpyAsync(dd, hin, static_cast<size_t>(k) * S, hipMemcpyHostToDevice, s));
+  const std::vector<uint8_t> &enc = cached_enc(k, n);
+  std::vector<const uint8_t *> in(k);
+  std::vector<uint8_t *> out(p);
+  std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(p, static_cast<size_t>(p) * S);
+  for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
+  for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
+  int rc = apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(), ins.data(),
+                 out.data(), outs.data(), S, 1, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dp, static_cast<size_t>(p) * S,
+                              hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  for (uint32_t i = 0; i < p; i++)
+    std::memcpy(parity_out[i], ctx->pin_out.p + static_cast<size_t>(i) * S, B);
+  return STORB_RS_OK;
+}
+
+int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+                    const uint32_t *share_idx, uint32_t nshares, size_t block,
+                    size_t padlen, uint8_t *out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (!shares || !share_idx || !out || block == 0 ||
+      padlen >= static_cast<size_t>(k) * block)
+    return fail(ctx, STORB_RS_EINVAL, "decode: bad arguments");
+  std::vector<uint32_t> slot_idx, slot_pos, missing;
+  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint8_t> coef;
+  rc = decode_rows(ctx, k, n, slot_idx, coef, missing);
+  if (rc) return rc;
+  const size_t outlen = static_cast<size_t>(k) * block - padlen;
+  auto put = [&](uint32_t row, const uint8_t *src) {
+    const size_t off = static_cast<size_t>(row) * block;
+    if (off < outlen) std::memcpy(out + off, src, std::min(block, outlen - off));
+  };
+  for (uint32_t s = 0; s < k; s++)
+    if (slot_idx[s] < k) put(s, shares[slot_pos[s]]);
+  if (missing.empty()) return STORB_RS_OK;  // all data shares present
+  const size_t S = round_up(block, kAlign);
+  const uint32_t e = static_cast<uint32_t>(missing.size());
+  DeviceGuard g(ctx->device);
+  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(e) * S));
+  HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + e) * S));
+  for (uint32_t c = 0; c < k; c++) {
+    std::memcpy(ctx->pin_in.p + static_cast<size_t>(c) * S, shares[slot_pos[c]], block);
+    std::memset(ctx->pin_in.p + static_cast<size_t>(c) * S + block, 0, S - block);
+  }
+  hipStream_t s = ctx->stream;
+  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
+  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                              hipMemcpyHostToDevice, s));
+  std::vector<const uint8_t *> in(k);
+  std::vector<uint8_t *> o(e);
+  std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(e, static_cast<size_t>(e) * S);
+  for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
+  for (uint32_t r = 0; r < e; r++) o[r] = dout + static_cast<size_t>(r) * S;
+  rc = apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(e) * S,
+                              hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  for (uint32_t r = 0; r < e; r++) put(missing[r], ctx->pin_out.p + static_cast<size_t>(r) * S);
+  return STORB_RS_OK;
+}
+
+// Pipelined batch encode: two pinned in/out buffer pairs and two streams.
+// While the GPU copies and encodes batch i, the host packs batch i+1 and
+// unpacks batch i-1 (hipMemcpyAsync from pinned memory is a true DMA).
+int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                           size_t chunk_len, uint32_t nchunks, uint8_t *parity_out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (chunk_len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
+  const uint32_t p = n - k;
+  if (p == 0 || nchunks == 0) return STORB_RS_OK;
+  if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  const size_t B = (chunk_len + k - 1) / k;
+  const size_t S = round_up(B, kAlign);
+  const bool packed = (S == B) && (B * k == chunk_len);
+  // ~64 MiB of input per batch keeps both DMA directions busy.
+  const size_t per = static_cast<size_t>(k) * S;
+  uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
+  batch = std::min(batch, nchunks);
+  DeviceGuard g(ctx->device);
+  for (int b = 0; b < 2; b++) {
+    HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
+    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch));
+    HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch));
+  }
+  const std::vector<uint8_t> &enc = cached_enc(k, n);
+  const Tables *t = nullptr;
+  int rc = get_tables(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, ctx->pipe[0], &t);
+  if (rc) return rc;
+  const uint32_t nb = (nchunks + batch - 1) / batch;
+  auto unpack = [&](uint32_t bi) {
+    const int b = bi & 1;
+    const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
+    if (S == B) {
+      std::memcpy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
+                  static_cast<size_t>(cn) * p * B);
+    } else {
+      for (uint32_t c = 0; c < cn; c++)
+        for (uint32_t i = 0; i < p; i++)
+          std::memcpy(parity_out + ((static_cast<size_t>(c0) + c) * p + i) * B,
+                      ctx->pipe_out[b].p + (static_cast<size_t>(c) * p + i) * S, B);
+    }
+  };
+  for (uint32_t bi = 0; bi < nb; bi++) {
+    const int b = bi & 1;
+    hipStream_t s = ctx->pipe[b];
+    if (bi >= 2) {  // buffer pair b is free once batch bi-2 has landed
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      unpack(bi - 2);
+    }
+    const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
+    uint8_t *hin = ctx->pipe_in[b].p;
+    if (packed) {
+      std::memcpy(hin, data + static_cast<size_t>(c0) * chunk_len, per * cn);
+    } else {
+      for (uint32_t c = 0; c < cn; c++) {
+        const uint8_t *src = data + (static_cast<size_t>(c0) + c) * chunk_len;
+        for (uint32_t j = 0; j < k; j++) {
+          const size_t off = static_cast<size_t>(j) * B;
+          const size_t cnt = off < chunk_len ? std::min(B, chunk_len - off) : 0;
+          uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(j) * S;
+          if (cnt) std::memcpy(dst, src + off, cnt);
+          std::memset(dst + cnt, 0, S - cnt);
+        }
+      }
+    }
+    uint8_t *dd = ctx->pipe_dev[b].p;
+    uint8_t *dp = dd + per * batch;
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
+    std::vector<const uint8_t *> in(k);
+    std::vector<uint8_t *> out(p);
+    std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
+    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
+    for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
+    rc = apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(), ins.data(),
+               out.data(), outs.data(), S, cn, s);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dp, static_cast<size_t>(p) * S * cn,
+                                hipMemcpyDeviceToHost, s));
+  }
+  for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[bi & 1]));
+    unpack(bi);
+  }
+  return STORB_RS_OK;
+}
+
+}  // extern "C"

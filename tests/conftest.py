@@ -1,0 +1,24 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device")
+    config.addinivalue_line("markers", "slow: full BASELINE-size cases")
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    from storb_amd import _lib
+    import torch
+    c = _lib.Context(0)
+    # Launch on torch's current stream so torch ops in the tests are ordered
+    # with the library's kernels.
+    c.default_stream = torch.cuda.current_stream(0).cuda_stream
+    yield c
+    c.close()
