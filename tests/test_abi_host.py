@@ -1,0 +1,103 @@
+"""C ABI library: loads, exports every declared symbol, host logic is right.
+
+No GPU compute here: only the host-side entry points (parameter checks,
+generator matrix, sizing) are called, plus the no-device error path.
+"""
+import ctypes
+import os
+import random
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import coracle as co
+from storb_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "storb_rs.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(storb_\w+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for f in ["storb_rs_ctx_create", "storb_rs_encode", "storb_rs_decode",
+              "storb_rs_encode_batch_dev", "storb_rs_decode_batch_dev", "storb_rs_apply_dev",
+              "storb_piece_length", "storb_get_k_and_m", "storb_rs_strerror"]:
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (storb_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_is_gfx950_code():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_product_never_imports_the_oracle():
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "storb_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.sub(r"(#|//).*", "", text).replace(
+                    "oracle/", ""), f"{f} references the oracle"
+
+
+def test_version_and_strerror():
+    assert "gfx950" in _lib.version()
+    L = _lib.lib()
+    for code in range(6):
+        assert L.storb_rs_strerror(code)
+
+
+def test_check_params_matches_zfec_rules():
+    for k, n, ok in [(1, 1, True), (1, 2, True), (4, 6, True), (256, 256, True), (0, 1, False),
+            (0, 0, False), (3, 2, False), (2, 257, False), (1, 0, False)]:
+        assert _lib.check_params(k, n) is ok, (k, n)
+
+
+def test_product_generator_matches_oracle():
+    # The product builds its generator independently (storb_amd/csrc/gf256.hpp).
+    for k in range(1, 34):
+        for n in range(k, min(k + 20, 257)):
+            assert np.array_equal(_lib.enc_matrix(k, n), co.enc_matrix(k, n)), (k, n)
+    for k, n in [(64, 96), (128, 192), (200, 256), (255, 256), (1, 256)]:
+        assert np.array_equal(_lib.enc_matrix(k, n), co.enc_matrix(k, n)), (k, n)
+    with pytest.raises(_lib.StorbRsError):
+        _lib.enc_matrix(0, 3)
+
+
+def test_block_size():
+    for k, L in [(1, 13), (4, 1 << 20), (4, 10), (3, 1), (7, 100)]:
+        assert _lib.block_size(k, L) == -(-L // k)
+
+
+def test_sizing_matches_oracle():
+    rng = random.Random(4)
+    for L in [0, 1, 2, 9, 13, 16383, 16384, 16385] + [rng.randrange(1, 1 << 50) for _ in range(3000)]:
+        assert _lib.piece_length(L) == co.piece_length(L), L
+        if L:
+            assert _lib.get_k_and_m(L) == co.get_k_and_m(L), L
+    assert _lib.piece_length(1000, 4096, 8192) == co.piece_length(1000, 4096, 8192)
+
+
+def test_no_device_is_an_error_not_a_fallback():
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(_lib.StorbRsError) as e:
+        _lib.Context(-1)
+    assert e.value.code == _lib.ENODEV
