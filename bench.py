@@ -5,7 +5,8 @@ Metric (BASELINE.json): "GiB/s device-resident RS encode+decode, 1 MiB chunks
 k=4 m=2, at 1/2/4/8 GPUs". m=2 is the PARITY count there, i.e. Storb's
 k=4, m=6 (piece.rs:307-317 picks exactly that for a 1 MiB chunk).
 
-One step = one pass of the hot path over one batch resident in HBM:
+Default (--config 2, the line the driver records). One step = one pass of
+the hot path over one batch resident in HBM:
   encode: 1024 x 1 MiB chunks (k=4 data shards of 256 KiB -> 2 parity shards)
   decode: the same 1024 chunks with data shards {0, 1} erased (the RS(4,2)
           worst case), rebuilt in place from shares {2, 3, 4, 5}.
@@ -14,6 +15,11 @@ Each rank owns its own 1024 chunks (independent objects partition across
 GPUs, no collective on the data path): weak scaling. The 2 GiB per step
 (+1 GiB parity) is well past the 256 MiB Infinity Cache, so the kernels
 stream from HBM.
+
+Other BASELINE configs (not the driver's line):
+  --config 3  RS(8,4) [storb k=8,m=12] decode, 4096 x 256 KiB, erased {0,3,5}
+  --config 4  10 000 x 1 MiB objects encoded, object i on rank i mod N
+              (strong scaling: total work fixed)
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
@@ -34,7 +40,7 @@ import torch.distributed as dist
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-from storb_amd import _lib  # noqa: E402
+from storb_amd import _lib, partition  # noqa: E402
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -47,8 +53,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--chunks", type=int, default=1024, help="1 MiB chunks per GPU")
-    p.add_argument("--chunk-bytes", type=int, default=1 << 20)
+    p.add_argument("--config", type=int, choices=[2, 3, 4], default=2)
+    p.add_argument("--chunks", type=int, default=None, help="chunks per GPU (config 2/3)")
+    p.add_argument("--objects", type=int, default=10000, help="total objects (config 4)")
     p.add_argument("--kernel", choices=["perm", "lds"], default="perm")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (0 disables)")
@@ -57,47 +64,53 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(k, n, chunk_bytes, erased, seconds):
+def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=True):
     """Reference CPU path (C restatement of zfec, oracle/) on this host.
 
     Single thread, like the reference: upload.rs:418-420 encodes one object's
     chunks sequentially in one task and download.rs:505-529 decodes them
-    sequentially. Sample: distinct splitmix chunks, encode + decode with the
-    same erasure, repeated until `seconds` of CPU time are spent.
+    sequentially. Sample: 8 distinct splitmix chunks of the benchmark's
+    shape, cycled until `seconds` of CPU time are spent.
     """
     from oracle import coracle  # test infrastructure: the baseline, never the product
 
-    B = chunk_bytes // k
     survivors = [i for i in range(n) if i not in erased][:k]
     sample = [coracle.splitmix_bytes(SEED_BASE + i, chunk_bytes) for i in range(8)]
+    prepared = [coracle.encode(k, n, d) for d in sample]
     done = 0
     t0 = time.perf_counter()
     while True:
-        data = sample[done % len(sample)]
-        shares, B, pad = coracle.encode(k, n, data)
-        rec = coracle.decode(k, n, [shares[i] for i in survivors], survivors, B, pad)
-        if done < len(sample) and rec != data.tobytes():
-            raise SystemExit("CPU baseline round trip failed")
+        i = done % len(sample)
+        if do_encode:
+            shares, B, pad = coracle.encode(k, n, sample[i])
+        else:
+            shares, B, pad = prepared[i]
+        if do_decode:
+            rec = coracle.decode(k, n, [shares[s] for s in survivors], survivors, B, pad)
+            if done < len(sample) and rec != sample[i].tobytes():
+                raise SystemExit("CPU baseline round trip failed")
         done += 1
         if time.perf_counter() - t0 >= seconds:
             break
     el = time.perf_counter() - t0
+    legs = int(do_encode) + int(do_decode)
+    what = "+".join(x for x, on in (("encode", do_encode), ("decode", do_decode)) if on)
     return {
-        "value": round(2 * done * chunk_bytes / GIB / el, 4),
+        "value": round(legs * done * chunk_bytes / GIB / el, 4),
         "unit": "GiB/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"{done} x encode+decode of 1 MiB chunks (k=4,n=6, erased {sorted(erased)}), "
-                   f"{el:.1f} s, 1 thread, scalar table-driven zfec restatement -O2; "
-                   f"host {platform.processor() or platform.machine()}, "
-                   f"{os.cpu_count()} logical CPUs visible"),
+        "sample": (f"{done} x {what} of {chunk_bytes >> 10} KiB chunks (k={k},n={n}"
+                   f"{', erased ' + str(sorted(erased)) if do_decode else ''}), {el:.1f} s, "
+                   f"1 thread, scalar table-driven zfec restatement -O2 (oracle/); host "
+                   f"{platform.machine()}, {os.cpu_count()} logical CPUs visible"),
     }
 
 
 def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256):
     """PCIe-inclusive encode: host bytes in, parity out (pinned pipeline)."""
-    host = np.empty(nchunks * chunk_bytes, dtype=np.uint8)
-    host[:] = np.frombuffer(np.random.default_rng(7).bytes(host.size), dtype=np.uint8)
+    host = np.frombuffer(np.random.default_rng(7).bytes(nchunks * chunk_bytes),
+                         dtype=np.uint8).copy()
     ctx.encode_chunks(k, n, host, chunk_bytes, nchunks)  # warm
     t0 = time.perf_counter()
     reps = 3
@@ -107,6 +120,82 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256):
     return {"value": round(reps * nchunks * chunk_bytes / GIB / el, 3), "unit": "GiB/s",
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB pageable "
                     "host chunks -> pinned H2D -> encode -> D2H parity, 2 streams"}
+
+
+class Workload:
+    """Device-resident buffers + the launches of one step."""
+
+    def __init__(self, a, ctx, dev, sp, rank, world):
+        self.ctx, self.sp = ctx, sp
+        c = a.config
+        if c == 2:
+            self.k, self.n, chunk, self.erased = 4, 6, 1 << 20, [0, 1]
+            N = a.chunks or 1024
+            seed0 = SEED_BASE + rank * N
+            self.legs = ("encode", "decode")
+            self.metric = METRIC
+            self.scaling = "weak"
+            self.workload = (f"RS(k=4,m=2) [storb k=4,m=6] encode + decode(erased [0, 1]) "
+                             f"of {N} x 1 MiB chunks per GPU, device-resident")
+        elif c == 3:
+            self.k, self.n, chunk, self.erased = 8, 12, 256 << 10, [0, 3, 5]
+            N = a.chunks or 4096
+            seed0 = SEED_BASE + rank * N
+            self.legs = ("decode",)
+            self.metric = ("GiB/s device-resident RS decode, 256 KiB chunks k=8 m=4, "
+                           "3 data shards erased")
+            self.scaling = "weak"
+            self.workload = (f"RS(k=8,m=4) [storb k=8,m=12] decode, erased [0, 3, 5], "
+                             f"survivors first 8 by index, {N} x 256 KiB chunks per GPU")
+        else:
+            self.k, self.n, chunk, self.erased = 4, 6, 1 << 20, []
+            mine = partition.objects_for_rank(a.objects, rank, world)
+            N = len(mine)
+            seed0 = None  # object i gets seed SEED_BASE + i (see _fill_strided)
+            self.legs = ("encode",)
+            self.metric = ("GiB/s batched RS(k=4,m=2) encode of 10 000 independent 1 MiB "
+                           "objects, round-robin over GPUs")
+            self.scaling = "strong"
+            self.workload = (f"{a.objects} x 1 MiB objects, object i on rank i mod {world}; "
+                             f"this rank {N} objects, one batched launch per step")
+        self.chunk, self.N = chunk, N
+        k, n = self.k, self.n
+        self.B = chunk // k
+        self.survivors = [i for i in range(n) if i not in self.erased][:k]
+        self.data = torch.empty(N * k * self.B, dtype=torch.uint8, device=dev)
+        self.parity = torch.empty(N * (n - k) * self.B, dtype=torch.uint8, device=dev)
+        self.dptr, self.pptr = self.data.data_ptr(), self.parity.data_ptr()
+        if c == 4:
+            self._fill_strided(rank, world)
+        else:
+            ctx.fill_splitmix_dev(self.dptr, chunk, N, chunk, seed0, stream=sp)
+        if "decode" in self.legs and "encode" not in self.legs:
+            self.encode()  # config 3 needs parity to decode from
+
+    def _fill_strided(self, rank, world):
+        # One launch per object keeps the seed = SEED_BASE + global object index
+        # exact; only done once at setup.
+        for j in range(self.N):
+            i = rank + j * world
+            self.ctx.fill_splitmix_dev(self.dptr + j * self.chunk, self.chunk, 1, self.chunk,
+                                       SEED_BASE + i, stream=self.sp)
+
+    def encode(self):
+        self.ctx.encode_batch_dev(self.k, self.n, self.B, self.N, self.dptr, self.pptr,
+                                  stream=self.sp)
+
+    def decode(self):
+        self.ctx.decode_batch_dev(self.k, self.n, self.B, self.N, self.survivors, self.dptr,
+                                  self.pptr, self.dptr, stream=self.sp)
+
+    def alg_bytes(self, leg):
+        # SURVEY 8(d): encode reads k*B, writes (n-k)*B per stripe; decode with
+        # e erased data shards reads k*B and writes e*B.
+        k, n, B, N = self.k, self.n, self.B, self.N
+        if leg == "encode":
+            return N * n * B
+        e = sum(1 for x in self.erased if x < k)
+        return N * (k + e) * B
 
 
 def main():
@@ -119,99 +208,80 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    k, n = 4, 6
-    erased = {0, 1}
-    survivors = [i for i in range(n) if i not in erased][:k]
-    chunk = a.chunk_bytes
-    B = chunk // k
-    assert chunk % k == 0 and B % 16 == 0
-    N = a.chunks
-
     ctx = _lib.Context(local)
     ctx.set_kernel(_lib.KERNEL_LDS if a.kernel == "lds" else _lib.KERNEL_PERM)
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
-
-    data = torch.empty(N * k * B, dtype=torch.uint8, device=dev)
-    parity = torch.empty(N * (n - k) * B, dtype=torch.uint8, device=dev)
-    dptr, pptr = data.data_ptr(), parity.data_ptr()
-    with torch.cuda.stream(stream):
-        ctx.fill_splitmix_dev(dptr, chunk, N, chunk, SEED_BASE + rank * N, stream=sp)
+    w = Workload(a, ctx, dev, sp, rank, world)
     stream.synchronize()
 
-    def encode():
-        ctx.encode_batch_dev(k, n, B, N, dptr, pptr, stream=sp)
-
-    def decode():
-        ctx.decode_batch_dev(k, n, B, N, survivors, dptr, pptr, dptr, stream=sp)
-
-    if not a.no_check:
+    if not a.no_check and w.erased:
         # Self-consistency at full size: wipe the erased shards, rebuild them
         # in place from parity, compare with the pristine copy. Bit-exactness
         # against the oracle is covered by tests/test_gpu_parity.py.
-        ref = data.clone()
-        encode()
-        view = data.view(N, k, B)
+        ref = w.data.clone()
+        w.encode()
+        view = w.data.view(w.N, w.k, w.B)
         with torch.cuda.stream(stream):
-            for e in erased:
-                view[:, e].zero_()
-        decode()
+            for e in w.erased:
+                if e < w.k:
+                    view[:, e].zero_()
+        w.decode()
         stream.synchronize()
-        if not torch.equal(data, ref):
+        if not torch.equal(w.data, ref):
             raise SystemExit("decode round trip mismatch")
         del ref
 
+    legs = [getattr(w, leg) for leg in w.legs]
     for _ in range(a.warmup):
-        encode()
-        decode()
+        for f in legs:
+            f()
     stream.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(legs) + 1)]
+          for _ in range(a.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        e0, e1, e2 = ev[i]
-        e0.record(stream)
-        encode()
-        e1.record(stream)
-        decode()
-        e2.record(stream)
+        ev[i][0].record(stream)
+        for j, f in enumerate(legs):
+            f()
+            ev[i][j + 1].record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / a.steps
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / a.steps
+    leg_ms = [sum(e[j].elapsed_time(e[j + 1]) for e in ev) / a.steps for j in range(len(legs))]
+    units = w.N * w.chunk * len(legs)  # user bytes per step on this rank
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    user_bytes = 2 * N * chunk  # encoded + decoded user data per rank per step
-    value = world * a.steps * user_bytes / GIB / elapsed
-    # Algorithmic HBM bytes per launch: encode reads k*B and
-    # writes (n-k)*B per stripe; decode with e erased data shards reads k*B
-    # and writes e*B. Both launches are the same rs_apply_perm<4,2> kernel.
-    enc_alg = N * (k + (n - k)) * B
-    dec_alg = N * (k + len(erased)) * B
-    achieved = (enc_alg + dec_alg) / ((enc_ms + dec_ms) * 1e-3) / 1e9
+        t = torch.tensor([elapsed, float(units)], dtype=torch.float64, device=dev)
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed, units_all = float(tmax.item()), float(tsum.item())
+    else:
+        units_all = float(units)
+    value = a.steps * units_all / GIB / elapsed
+    alg = {leg: w.alg_bytes(leg) for leg in w.legs}
+    achieved = sum(alg.values()) / (sum(leg_ms) * 1e-3) / 1e9
 
     traffic = None
     tpath = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
+    if a.config == 2 and os.path.exists(tpath):
         try:
             t = json.load(open(tpath))
-            if t.get("kernel") == a.kernel and t.get("chunks") == N and t.get("chunk_bytes") == chunk:
+            if (t.get("kernel") == a.kernel and t.get("chunks") == w.N
+                    and t.get("chunk_bytes") == w.chunk):
                 traffic = t.get("bytes_per_launch")
         except Exception:
             traffic = None
 
     out = {
-        "metric": METRIC,
+        "metric": w.metric,
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -219,16 +289,16 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": w.scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: splitmix64 bytes, seed 0x5709B + object index, resident in HBM",
         "config": {
-            "workload": (f"RS(k=4,m=2) [storb k=4,m=6] encode + decode(erased {sorted(erased)}) "
-                         f"of {N} x {chunk >> 20} MiB chunks per GPU, device-resident"),
-            "k": k, "m_total": n, "parity": n - k, "chunk_bytes": chunk,
-            "shard_bytes": B, "chunks_per_gpu": N, "erased": sorted(erased),
-            "survivors": survivors, "kernel": a.kernel,
+            "workload": w.workload,
+            "baseline_config": a.config,
+            "k": w.k, "m_total": w.n, "parity": w.n - w.k, "chunk_bytes": w.chunk,
+            "shard_bytes": w.B, "chunks_per_gpu": w.N, "erased": w.erased,
+            "survivors": w.survivors if w.erased else None, "kernel": a.kernel,
             "parallelism": f"independent objects, {world} GPU(s), no collectives",
         },
         "roofline": {
@@ -238,18 +308,20 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "rs_apply_perm<4,2,exact> (encode and decode launches)",
-            "encode_ms": round(enc_ms, 4),
-            "decode_ms": round(dec_ms, 4),
-            "alg_bytes_per_launch": {"encode": enc_alg, "decode": dec_alg},
+            "kernel": f"rs_apply_{a.kernel}<{min(w.k, 32)},"
+                      f"{(w.n - w.k) if 'encode' in w.legs else len(w.erased)}> (all launches)",
+            "leg_ms": {leg: round(ms, 4) for leg, ms in zip(w.legs, leg_ms)},
+            "alg_bytes_per_launch": alg,
         },
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
         if a.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(k, n, chunk, erased, a.cpu_seconds)
-        if not a.no_host_path:
-            out["pcie_inclusive"] = host_path_rate(ctx, k, n, chunk)
+            out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.erased), a.cpu_seconds,
+                                               do_encode="encode" in w.legs,
+                                               do_decode="decode" in w.legs)
+        if not a.no_host_path and a.config == 2:
+            out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -105,7 +105,8 @@ int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
 /* Stripe s, data share j lives at d_data + s*data_stride + j*block; parity
  * share p at d_parity + s*parity_stride + p*block. Strides of 0 mean the
  * packed defaults k*block and (n-k)*block. Asynchronous on `hip_stream`
- * (a hipStream_t; NULL = the context's own stream). */
+ * (a hipStream_t; NULL = the HIP null stream, which orders with the
+ * device's legacy default stream). */
 int storb_rs_encode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                               size_t block, uint32_t nstripes,
                               const uint8_t *d_data, size_t data_stride,

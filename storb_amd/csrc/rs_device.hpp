@@ -35,99 +35,190 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 static constexpr int kThreads = 256;
 
+// Launch shape per (k, r) bucket: T threads per block, U dwordx4 columns
+// per lane, BAR = sched_barrier between coefficients (needed only where the
+// compiler would otherwise hoist tables/selectors past the register file).
+// Chosen by measurement (tools/kbench_tune.hip, DESIGN.md "Tuning").
+// G = input shares per load group (double-buffered); TL = stage the
+// k*RM nibble tables in LDS at block start and read them as broadcast
+// ds_reads instead of s_loads.
+template <int KM, int RM>
+struct Tune {
+  static constexpr int T = 256;
+  static constexpr int U = 1;
+  static constexpr bool BAR = false;
+  static constexpr int G = KM < 8 ? KM : 8;
+  static constexpr bool TL = KM >= 8;
+};
+
 template <int KM>
-struct Unroll {
-  // Columns per lane: enough dwordx4 loads in flight without blowing the
-  // register budget as k grows.
+struct Unroll {  // LDS comparison kernel
   static constexpr int U = KM <= 4 ? 2 : 1;
 };
 
-__device__ __forceinline__ uint32_t gf_mul_perm(const PermTab &t, uint32_t s0,
-                                                uint32_t s1, uint32_t s2) {
-  return __builtin_amdgcn_perm(t.t0hi, t.t0lo, s0) ^
-         __builtin_amdgcn_perm(t.t1hi, t.t1lo, s1) ^
-         __builtin_amdgcn_perm(0u, t.t2, s2);
+// a ^ b ^ c in one v_bitop3_b32 (gfx950; truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-template <int KM, int RM, bool EXACT, bool GUARD>
-__device__ __forceinline__ void perm_tile(const ApplyArgs &a, uint32_t k,
-                                          uint32_t r, uint32_t cols,
-                                          uint32_t stripe, uint32_t c0) {
-  constexpr int U = Unroll<KM>::U;
-  u32x4 x[KM][U];
+__device__ __forceinline__ uint32_t gf_mul_perm(const PermTab &t, uint32_t s0,
+                                                uint32_t s1, uint32_t s2) {
+  return xor3(__builtin_amdgcn_perm(t.t0hi, t.t0lo, s0),
+              __builtin_amdgcn_perm(t.t1hi, t.t1lo, s1),
+              __builtin_amdgcn_perm(0u, t.t2, s2));
+}
+
+// acc ^ c*x with the three lookups folded in two XOR instructions.
+__device__ __forceinline__ uint32_t gf_madd_perm(uint32_t acc, const PermTab &t,
+                                                 uint32_t s0, uint32_t s1, uint32_t s2) {
+  acc = xor3(acc, __builtin_amdgcn_perm(t.t0hi, t.t0lo, s0),
+             __builtin_amdgcn_perm(t.t1hi, t.t1lo, s1));
+  return acc ^ __builtin_amdgcn_perm(0u, t.t2, s2);
+}
+
+// Shards are streamed exactly once: non-temporal loads and stores keep them
+// from churning L2/MALL (measured +8-10 % on RS(4,2), tools/kbench.hip,
+// reaching the copy ceiling of the same access shape).
+__device__ __forceinline__ u32x4 ld_stream(const u32x4 *p) {
+  return __builtin_nontemporal_load(p);
+}
+__device__ __forceinline__ void st_stream(u32x4 *p, u32x4 v) {
+  __builtin_nontemporal_store(v, p);
+}
+
+// Inputs are consumed in groups of up to 8 shares; the next group's
+// dwordx4 loads are issued before the current group is multiplied (double
+// buffer), so a k = 32 tile needs 2 x 8 input registers per column instead
+// of 32.
+template <int KM, int G, int T, int U, bool GUARD>
+__device__ __forceinline__ void load_group(const ApplyArgs &a, uint32_t k, uint32_t cols,
+                                           uint32_t stripe, uint32_t c0, int g,
+                                           u32x4 (&dst)[G][U]) {
 #pragma unroll
-  for (int j = 0; j < KM; j++) {
-    if (EXACT || j < static_cast<int>(k)) {
-      const u32x4 *p = reinterpret_cast<const u32x4 *>(
-          a.in[j] + static_cast<uint64_t>(stripe) * a.in_stride[j]);
+  for (int jj = 0; jj < G; jj++) {
+    const int j = g * G + jj;
+    if (j >= static_cast<int>(k)) continue;
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(
+        a.in[j] + static_cast<uint64_t>(stripe) * a.in_stride[j]);
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t c = c0 + u * kThreads;
-        if (GUARD)
-          x[j][u] = c < cols ? p[c] : u32x4{0, 0, 0, 0};
-        else
-          x[j][u] = p[c];
-      }
+    for (int u = 0; u < U; u++) {
+      const uint32_t c = c0 + u * T;
+      if (GUARD)
+        dst[jj][u] = c < cols ? ld_stream(p + c) : u32x4{0, 0, 0, 0};
+      else
+        dst[jj][u] = ld_stream(p + c);
     }
   }
+}
 
+// Register budget: the compiler would otherwise hoist every coefficient's
+// five table dwords and every input's selectors into VGPRs up front (254+
+// VGPRs and scratch spills at k = 8, r = 4). Per input the selectors are
+// computed once; per (row, input) the table is read from SGPRs right
+// before its v_perm_b32s, and a sched_barrier stops the hoisting.
+template <int KM, int RM, int T, int U, bool BAR, int G, bool GUARD>
+__device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tabs,
+                                          uint32_t k, uint32_t r, uint32_t cols,
+                                          uint32_t stripe, uint32_t c0) {
+  constexpr int NG = KM / G;
+  u32x4 buf[2][G][U];
   u32x4 acc[RM][U];
 #pragma unroll
   for (int i = 0; i < RM; i++)
 #pragma unroll
     for (int u = 0; u < U; u++) acc[i][u] = u32x4{0, 0, 0, 0};
 
+  load_group<KM, G, T, U, GUARD>(a, k, cols, stripe, c0, 0, buf[0]);
 #pragma unroll
-  for (int j = 0; j < KM; j++) {
-    if (!(EXACT || j < static_cast<int>(k))) continue;
+  for (int g = 0; g < NG; g++) {
+    if (g + 1 < NG)
+      load_group<KM, G, T, U, GUARD>(a, k, cols, stripe, c0, g + 1, buf[(g + 1) & 1]);
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int jj = 0; jj < G; jj++) {
+      const int j = g * G + jj;
+      if (j >= static_cast<int>(k)) continue;
+      uint32_t s0[U][4], s1[U][4], s2[U][4];
 #pragma unroll
-      for (int w = 0; w < 4; w++) {
-        const uint32_t d = x[j][u][w];
-        const uint32_t s0 = d & 0x07070707u;
-        const uint32_t s1 = (d >> 3) & 0x07070707u;
-        const uint32_t s2 = (d >> 6) & 0x03030303u;
+      for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int i = 0; i < RM; i++) {
-          if (!(EXACT || i < static_cast<int>(r))) continue;
-          const PermTab &t = a.ptab[i * k + j];
-          acc[i][u][w] ^= gf_mul_perm(t, s0, s1, s2);
+        for (int w = 0; w < 4; w++) {
+          const uint32_t d = buf[g & 1][jj][u][w];
+          s0[u][w] = d & 0x07070707u;
+          s1[u][w] = (d >> 3) & 0x07070707u;
+          s2[u][w] = (d >> 6) & 0x03030303u;
         }
-      }
+      // Tables are stored [input][RM rows], rows >= r zero-padded by the
+      // host: no per-row guard, so input j is one basic block in which all
+      // RM table loads issue together and overlap the v_perm work (per-row
+      // guards made every coefficient wait out a full load latency).
+      PermTab t[RM];
+#pragma unroll
+      for (int i = 0; i < RM; i++) t[i] = tabs[j * RM + i];
+#pragma unroll
+      for (int i = 0; i < RM; i++)
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+          for (int w = 0; w < 4; w++)
+            acc[i][u][w] = gf_madd_perm(acc[i][u][w], t[i], s0[u][w], s1[u][w], s2[u][w]);
+      if constexpr (BAR) __builtin_amdgcn_sched_barrier(0);
     }
   }
 
 #pragma unroll
   for (int i = 0; i < RM; i++) {
-    if (!(EXACT || i < static_cast<int>(r))) continue;
+    if (i >= static_cast<int>(r)) continue;
     u32x4 *q = reinterpret_cast<u32x4 *>(
         a.out[i] + static_cast<uint64_t>(stripe) * a.out_stride[i]);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t c = c0 + u * kThreads;
+      const uint32_t c = c0 + u * T;
       if (!GUARD || c < cols) {
         u32x4 v = acc[i][u];
         if (a.accumulate) v ^= q[c];
-        q[c] = v;
+        st_stream(q + c, v);
       }
     }
   }
 }
 
-template <int KM, int RM, bool EXACT>
-__global__ __launch_bounds__(kThreads) void rs_apply_perm(const ApplyArgs a) {
-  constexpr uint32_t TILE = kThreads * Unroll<KM>::U;
-  const uint32_t k = EXACT ? KM : a.k;
-  const uint32_t r = EXACT ? RM : a.r;
+// k <= KM and r <= RM at run time. The j < k / i < r guards are uniform
+// scalar branches; they also split the body into basic blocks, which keeps
+// the scheduler from hoisting every table load and selector (a guard-free
+// "exact" specialisation measured 181-256 VGPRs and scratch spills).
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL>
+__global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
+  constexpr uint32_t TILE = T * U;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + TILE - 1) / TILE;
   const uint32_t stripe = blockIdx.x / tps;
   const uint32_t base = (blockIdx.x - stripe * tps) * TILE;
+  const PermTab *tabs = a.ptab;
+  if constexpr (TL) {
+    __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * RM];
+    const uint32_t n16 = a.k * RM * (sizeof(PermTab) / 16);
+    for (uint32_t t = threadIdx.x; t < n16; t += T)
+      reinterpret_cast<u32x4 *>(lds_ptab)[t] = reinterpret_cast<const u32x4 *>(a.ptab)[t];
+    __syncthreads();
+    tabs = lds_ptab;
+  }
   if (base + TILE <= cols)
-    perm_tile<KM, RM, EXACT, false>(a, k, r, cols, stripe, base + threadIdx.x);
+    perm_tile<KM, RM, T, U, BAR, G, false>(a, tabs, a.k, a.r, cols, stripe,
+                                               base + threadIdx.x);
   else
-    perm_tile<KM, RM, EXACT, true>(a, k, r, cols, stripe, base + threadIdx.x);
+    perm_tile<KM, RM, T, U, BAR, G, true>(a, tabs, a.k, a.r, cols, stripe,
+                                              base + threadIdx.x);
+}
+
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL>
+hipError_t launch_perm(const ApplyArgs &a, hipStream_t s) {
+  const uint64_t cols = a.block >> 4;
+  const uint64_t blocks = ((cols + T * U - 1) / (T * U)) * a.nstripes;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL>), dim3(blocks), dim3(T), 0,
+                     s, a);
+  return hipGetLastError();
 }
 
 template <int KM, int RM>
@@ -142,7 +233,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_lds(const ApplyArgs a) {
   const uint32_t c0 = (blockIdx.x - stripe * tps) * TILE + threadIdx.x;
 
   // Stage the r*k product tables (256 B each) into LDS, 16 B per lane.
-  const uint32_t tab16 = r * k * 16;
+  const uint32_t tab16 = a.tab_rows * k * 16;
   for (uint32_t t = threadIdx.x; t < tab16; t += kThreads)
     reinterpret_cast<u32x4 *>(lds_tab)[t] =
         reinterpret_cast<const u32x4 *>(a.btab)[t];
@@ -156,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_lds(const ApplyArgs a) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const uint32_t c = c0 + u * kThreads;
-        x[j][u] = c < cols ? p[c] : u32x4{0, 0, 0, 0};
+        x[j][u] = c < cols ? ld_stream(p + c) : u32x4{0, 0, 0, 0};
       }
     }
   }
@@ -179,7 +270,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_lds(const ApplyArgs a) {
 #pragma unroll
         for (int i = 0; i < RM; i++) {
           if (i >= static_cast<int>(r)) continue;
-          const uint8_t *row = lds_tab + (i * k + j) * 256u;
+          const uint8_t *row = lds_tab + (j * a.tab_rows + i) * 256u;
           acc[i][u][w] ^= static_cast<uint32_t>(row[d & 0xFF]) |
                           static_cast<uint32_t>(row[(d >> 8) & 0xFF]) << 8 |
                           static_cast<uint32_t>(row[(d >> 16) & 0xFF]) << 16 |
@@ -200,16 +291,10 @@ __global__ __launch_bounds__(kThreads) void rs_apply_lds(const ApplyArgs a) {
       if (c < cols) {
         u32x4 v = acc[i][u];
         if (a.accumulate) v ^= q[c];
-        q[c] = v;
+        st_stream(q + c, v);
       }
     }
   }
-}
-
-inline int pow2_bucket(uint32_t v) {  // smallest power of two >= v
-  int b = 1;
-  while (b < static_cast<int>(v)) b <<= 1;
-  return b;
 }
 
 template <int KM>
@@ -221,24 +306,20 @@ inline uint64_t tile_blocks(const ApplyArgs &a) {
 
 template <int KM, int RM>
 hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
-  const uint64_t blocks = tile_blocks<KM>(a);
-  if (blocks == 0) return hipSuccess;
-  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  if (a.k == KM && a.r == RM)
-    hipLaunchKernelGGL((rs_apply_perm<KM, RM, true>), dim3(blocks), dim3(kThreads),
-                       0, s, a);
-  else
-    hipLaunchKernelGGL((rs_apply_perm<KM, RM, false>), dim3(blocks),
-                       dim3(kThreads), 0, s, a);
-  return hipGetLastError();
+  using C = Tune<KM, RM>;
+  return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL>(a, s);
 }
 
 template <int KM>
 hipError_t go_perm_r(const ApplyArgs &a, hipStream_t s) {
-  switch (pow2_bucket(a.r)) {
+  switch (rows_bucket(a.r)) {
     case 1: return go_perm<KM, 1>(a, s);
     case 2: return go_perm<KM, 2>(a, s);
+    case 3: return go_perm<KM, 3>(a, s);
     case 4: return go_perm<KM, 4>(a, s);
+    case 5: return go_perm<KM, 5>(a, s);
+    case 6: return go_perm<KM, 6>(a, s);
+    case 7: return go_perm<KM, 7>(a, s);
     case 8: return go_perm<KM, 8>(a, s);
     default: return go_perm<KM, 16>(a, s);
   }

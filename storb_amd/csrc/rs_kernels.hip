@@ -30,7 +30,7 @@ __global__ __launch_bounds__(kThreads) void rs_apply_bytes(const ApplyArgs a) {
 #pragma unroll
     for (int i = 0; i < kSlotR; i++)
       if (i < static_cast<int>(a.r))
-        acc[i] ^= gf_mul_perm(a.ptab[i * a.k + j], s0, s1, s2);
+        acc[i] ^= gf_mul_perm(a.ptab[j * a.tab_rows + i], s0, s1, s2);
   }
 #pragma unroll
   for (int i = 0; i < kSlotR; i++) {
@@ -79,7 +79,8 @@ bool vector_ok(const ApplyArgs &a) {
 }
 
 hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s) {
-  if (a.k == 0 || a.r == 0 || a.k > kSlotK || a.r > kSlotR)
+  if (a.k == 0 || a.r == 0 || a.k > kSlotK || a.r > kSlotR ||
+      a.tab_rows != static_cast<uint32_t>(rows_bucket(a.r)))
     return hipErrorInvalidValue;
   if (a.block == 0 || a.nstripes == 0) return hipSuccess;
   if (!vector_ok(a)) {

@@ -20,15 +20,28 @@ struct ApplyArgs {
   uint64_t in_stride[kSlotK];
   uint8_t *out[kSlotR];
   uint64_t out_stride[kSlotR];
-  const PermTab *ptab;  // r*k nibble tables, row-major [row][col]
-  const uint8_t *btab;  // r*k 256-byte product tables (LDS variant)
+  const PermTab *ptab;  // nibble tables [col][tab_rows], rows >= r zeroed
+  const uint8_t *btab;  // 256-byte product tables, same order (LDS variant)
   uint32_t k, r;
+  uint32_t tab_rows;    // row stride of both tables = rows_bucket(r)
   uint64_t block;       // bytes per share
   uint32_t nstripes;
   uint32_t accumulate;  // 1: out ^= result (column tiling), 0: out = result
 };
 
 enum class Variant { Perm = 1, Lds = 2 };
+
+// Smallest power of two >= v: the kernel bucket for k.
+inline int pow2_bucket(uint32_t v) {
+  int b = 1;
+  while (b < static_cast<int>(v)) b <<= 1;
+  return b;
+}
+
+// Kernel bucket for r output rows = the padded row count (tab_rows) of the
+// coefficient tables: exact up to 8 rows (no wasted v_perm work for the
+// odd erasure counts decode produces), 16 above.
+inline int rows_bucket(uint32_t r) { return r <= 8 ? static_cast<int>(r) : 16; }
 
 // True when every slot base / stride and the share size are 16-B aligned,
 // i.e. the dwordx4 kernels apply; otherwise the byte kernel runs.

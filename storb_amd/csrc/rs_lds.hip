@@ -10,7 +10,7 @@ hipError_t go_lds(const ApplyArgs &a, hipStream_t s) {
   const uint64_t blocks = tile_blocks<KM>(a);
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  const size_t lds = static_cast<size_t>(a.r) * a.k * 256;
+  const size_t lds = static_cast<size_t>(a.tab_rows) * a.k * 256;
   hipLaunchKernelGGL((rs_apply_lds<KM, RM>), dim3(blocks), dim3(kThreads), lds, s,
                      a);
   return hipGetLastError();
@@ -18,9 +18,10 @@ hipError_t go_lds(const ApplyArgs &a, hipStream_t s) {
 
 template <int KM>
 hipError_t go_lds_r(const ApplyArgs &a, hipStream_t s) {
-  switch (pow2_bucket(a.r)) {
+  switch (rows_bucket(a.r)) {
     case 1: return go_lds<KM, 1>(a, s);
     case 2: return go_lds<KM, 2>(a, s);
+    case 3:
     case 4: return go_lds<KM, 4>(a, s);
     default: return go_lds<KM, 8>(a, s);
   }

@@ -153,12 +153,14 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
   }
   if (ctx->tables.size() > 4096) ctx->tables.clear();
   auto t = std::make_unique<Tables>();
-  // Count coefficients per block in the same order the launcher walks.
+  // Blocks in the order the launcher walks them; each block's tables are
+  // [input][tab_rows] with tab_rows = rows_bucket(rows in block) and the
+  // padding rows left as zero tables (the kernels compute them unguarded).
   size_t total = 0;
   for (uint32_t rb = 0; rb < rows; rb += kSlotR)
     for (uint32_t cb = 0; cb < k; cb += kSlotK) {
       t->b_off.push_back(total);
-      total += static_cast<size_t>(std::min<uint32_t>(kSlotR, rows - rb)) *
+      total += static_cast<size_t>(rows_bucket(std::min<uint32_t>(kSlotR, rows - rb))) *
                std::min<uint32_t>(kSlotK, k - cb);
     }
   t->perm_bytes = round_up(total * sizeof(PermTab), 256);
@@ -171,10 +173,11 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
     for (uint32_t cb = 0; cb < k; cb += kSlotK, bi++) {
       const uint32_t rr = std::min<uint32_t>(kSlotR, rows - rb);
       const uint32_t kk = std::min<uint32_t>(kSlotK, k - cb);
+      const uint32_t rp = static_cast<uint32_t>(rows_bucket(rr));
       for (uint32_t i = 0; i < rr; i++)
         for (uint32_t j = 0; j < kk; j++) {
           const uint8_t c = coef[static_cast<size_t>(rb + i) * k + cb + j];
-          const size_t o = t->b_off[bi] + static_cast<size_t>(i) * kk + j;
+          const size_t o = t->b_off[bi] + static_cast<size_t>(j) * rp + i;  // [col][row]
           pt[o] = perm_tab(c);
           for (int x = 0; x < 256; x++) bt[o * 256 + x] = g.mul(c, static_cast<uint8_t>(x));
         }
@@ -212,6 +215,7 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
         a.out[i] = d_out[rb + i];
         a.out_stride[i] = out_stride[rb + i];
       }
+      a.tab_rows = static_cast<uint32_t>(rows_bucket(a.r));
       a.ptab = reinterpret_cast<const PermTab *>(t->dev) + t->b_off[bi];
       a.btab = t->dev + t->perm_bytes + t->b_off[bi] * 256;
       a.block = block;
@@ -282,8 +286,10 @@ int decode_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   return STORB_RS_OK;
 }
 
-hipStream_t pick_stream(storb_rs_ctx *ctx, void *s) {
-  return s ? reinterpret_cast<hipStream_t>(s) : ctx->stream;
+// NULL is the HIP null stream (ordered with the device's legacy default
+// stream, which is also PyTorch's default stream), not the context's own.
+hipStream_t pick_stream(storb_rs_ctx *, void *s) {
+  return reinterpret_cast<hipStream_t>(s);
 }
 
 }  // namespace

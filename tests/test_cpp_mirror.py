@@ -1,0 +1,35 @@
+"""The C++ host mirror (include/storb_piece.hpp) and its reference-test port.
+
+CPU: the test binary compiles and links against libstorb_rs.so.
+GPU: it runs (the Rust-style tests of piece.rs on the MI355X path).
+"""
+import os
+import subprocess
+
+import pytest
+
+from storb_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "test_piece.cpp")
+OUT = os.path.join(ROOT, "tests", "cpp", "_build", "test_piece")
+
+
+def build_binary():
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", OUT, SRC, f"-L{libdir}", "-lstorb_rs",
+                    f"-Wl,-rpath,{libdir}", "-lpthread"], check=True)
+    return OUT
+
+
+def test_cpp_mirror_compiles_and_links():
+    assert os.path.exists(build_binary())
+
+
+@pytest.mark.gpu
+def test_cpp_mirror_reference_tests_pass():
+    exe = build_binary()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all checks passed" in r.stdout

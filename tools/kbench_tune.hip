@@ -1,0 +1,203 @@
+// kbench_tune.hip -- pick the launch shape (threads T, dwordx4 columns per
+// lane U, sched_barrier BAR) of the product kernel rs_apply_perm per (k, r)
+// bucket, on the BASELINE shapes:
+//   W1  RS(4,2) encode     1024 x 1 MiB   (k=4,  r=2, B=256 KiB)   config 2
+//   W2  RS(8,4) decode e=3 4096 x 256 KiB (k=8,  r=3, B=32 KiB)    config 3
+//   W3  RS(16,8) encode    128 x 8 MiB    (k=16, r=8, B=512 KiB)   config 5 shape
+// Every variant's output is compared bit-exactly with the first variant's;
+// timings are interleaved rounds in one process (guide 5.4 rule 24).
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../storb_amd/csrc \
+//        kbench_tune.hip -o _build/kbench_tune
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "gf256.hpp"
+#include "rs_device.hpp"
+
+using namespace storb_rs;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,          \
+                   hipGetErrorString(e));                                      \
+      std::exit(1);                                                            \
+    }                                                                          \
+  } while (0)
+
+__global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = z ^ (z >> 31);
+  }
+}
+
+struct V {
+  std::string name;
+  std::function<hipError_t(const ApplyArgs &, hipStream_t)> fn;
+  std::vector<float> us;
+};
+
+struct W {
+  const char *name;
+  uint32_t k, r, n_stripes;
+  uint64_t B;
+  std::vector<V> vs;
+  bool inplace = false;  // decode layout of bench --config 3 (see below)
+};
+
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL = false>
+V mk() {
+  char buf[96];
+  std::snprintf(buf, sizeof buf, "<%d,%d> T=%d U=%d BAR=%d G=%d TL=%d", KM, RM, T, U, (int)BAR,
+                G, (int)TL);
+  return V{buf, [](const ApplyArgs &a, hipStream_t s) {
+             return launch_perm<KM, RM, T, U, BAR, G, TL>(a, s);
+           }, {}};
+}
+
+template <int KM, int RM>
+V product() {
+  using C = Tune<KM, RM>;
+  V v = mk<KM, RM, C::T, C::U, C::BAR, C::G, C::TL>();
+  v.name = "product " + v.name;
+  return v;
+}
+
+template <int KM, int RM>
+void add_all(std::vector<V> &v) {
+  constexpr int GM = KM < 8 ? KM : 8;
+  v.push_back(product<KM, RM>());
+  v.push_back(mk<KM, RM, 256, 1, false, GM, false>());
+  v.push_back(mk<KM, RM, 256, 1, true, GM, false>());
+  v.push_back(mk<KM, RM, 256, 1, false, GM, true>());
+  v.push_back(mk<KM, RM, 256, 1, true, GM, true>());
+  v.push_back(mk<KM, RM, 128, 1, true, GM, false>());
+  v.push_back(mk<KM, RM, 128, 1, true, GM, true>());
+  v.push_back(mk<KM, RM, 256, 2, true, GM, false>());
+  v.push_back(mk<KM, RM, 256, 2, true, GM, true>());
+  if constexpr (KM >= 8) {
+    v.push_back(mk<KM, RM, 256, 1, true, 4, false>());
+    v.push_back(mk<KM, RM, 256, 1, true, 4, true>());
+    v.push_back(mk<KM, RM, 64, 1, true, 4, true>());
+    v.push_back(mk<KM, RM, 128, 1, true, 4, true>());
+  }
+}
+
+int main(int argc, char **argv) {
+  const int rounds = argc > 1 ? std::atoi(argv[1]) : 5;
+  const int reps = 8;
+  std::vector<W> ws = {{"W1 RS(4,2) encode 1024 x 1 MiB", 4, 2, 1024, 256 << 10, {}},
+                       {"W2 RS(8,4) decode e=3 4096 x 256 KiB", 8, 3, 4096, 32 << 10, {}},
+                       {"W3 RS(16,8) encode 128 x 8 MiB", 16, 8, 128, 512 << 10, {}},
+                       {"W2i RS(8,4) decode e=3 in place (bench config 3 layout)", 8, 3, 4096,
+                        32 << 10, {}, true}};
+  add_all<4, 2>(ws[0].vs);
+  add_all<8, 3>(ws[1].vs);
+  add_all<16, 8>(ws[2].vs);
+  add_all<8, 3>(ws[3].vs);
+  ws[3].vs.push_back(mk<8, 4, 256, 1, false, 8, true>());  // previous pow2 bucket
+  ws[3].vs.back().name += " (r padded to 4)";
+  if (argc > 2) ws.erase(ws.begin(), ws.begin() + std::atoi(argv[2]));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto &w : ws) {
+    const uint64_t in_bytes = (uint64_t)w.n_stripes * w.k * w.B;
+    const uint64_t out_bytes = (uint64_t)w.n_stripes * w.r * w.B;
+    uint8_t *in, *out;
+    CK(hipMalloc(&in, in_bytes));
+    CK(hipMalloc(&out, w.inplace ? (uint64_t)w.n_stripes * 4 * w.B : out_bytes));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, in_bytes / 8, w.k);
+    if (w.inplace)  // random "parity" too: zero inputs raise the clock (DVFS)
+      hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)out,
+                         (uint64_t)w.n_stripes * 4 * w.B / 8, 77);
+    // coefficients: enc rows of (k, k+r) -- shape is what matters
+    const std::vector<uint8_t> enc = enc_matrix(w.k, w.k + w.r);
+    std::vector<PermTab> tabs;
+    const uint32_t rp = rows_bucket(w.r);  // [input][rows_bucket(r)], zero padded
+    for (uint32_t j = 0; j < w.k; j++)
+      for (uint32_t i = 0; i < rp; i++)
+        tabs.push_back(i < w.r ? perm_tab(enc[(w.k + i) * w.k + j]) : PermTab{});
+    PermTab *dt;
+    CK(hipMalloc(&dt, (size_t)w.k * 16 * sizeof(PermTab)));  // room for any padded variant
+    CK(hipMemcpy(dt, tabs.data(), tabs.size() * sizeof(PermTab), hipMemcpyHostToDevice));
+    ApplyArgs a{};
+    a.k = w.k;
+    a.r = w.r;
+    for (uint32_t j = 0; j < w.k; j++) {
+      a.in[j] = in + j * w.B;
+      a.in_stride[j] = w.k * w.B;
+    }
+    for (uint32_t i = 0; i < w.r; i++) {
+      a.out[i] = out + i * w.B;
+      a.out_stride[i] = w.r * w.B;
+    }
+    if (w.inplace) {
+      // survivors {1,2,4,6,7} from the data region (stride 8B) and parity
+      // {8,9,10} from the parity region (stride 4B); rebuilt {0,3,5} written
+      // into the data region: exactly decode_batch_dev(..., d_out = d_data).
+      const int surv[8] = {1, 2, 4, 6, 7, 8, 9, 10}, lost[3] = {0, 3, 5};
+      for (int j = 0; j < 8; j++) {
+        a.in[j] = surv[j] < 8 ? in + surv[j] * w.B : out + (surv[j] - 8) * w.B;
+        a.in_stride[j] = surv[j] < 8 ? 8 * w.B : 4 * w.B;
+      }
+      for (int i = 0; i < 3; i++) {
+        a.out[i] = in + lost[i] * w.B;
+        a.out_stride[i] = 8 * w.B;
+      }
+    }
+    a.ptab = dt;
+    a.tab_rows = rp;
+    a.block = w.B;
+    a.nstripes = w.n_stripes;
+    std::vector<uint8_t> ref(out_bytes), got(out_bytes);
+    for (size_t vi = 0; vi < w.vs.size() && !w.inplace; vi++) {
+      CK(hipMemset(out, 0, out_bytes));
+      CK(w.vs[vi].fn(a, s));
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(vi ? got.data() : ref.data(), out, out_bytes, hipMemcpyDeviceToHost));
+      if (vi && std::memcmp(got.data(), ref.data(), out_bytes)) {
+        std::printf("MISMATCH %s %s\n", w.name, w.vs[vi].name.c_str());
+        return 2;
+      }
+    }
+    for (int rd = 0; rd < rounds; rd++)
+      for (auto &v : w.vs) {
+        CK(v.fn(a, s));
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < reps; i++) CK(v.fn(a, s));
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.us.push_back(ms * 1000.f / reps);
+      }
+    const double bytes = (double)in_bytes + out_bytes;
+    std::printf("%s: %.3f GB algorithmic per launch\n", w.name, bytes / 1e9);
+    for (auto &v : w.vs) {
+      std::sort(v.us.begin(), v.us.end());
+      const float med = v.us[v.us.size() / 2];
+      std::printf("  %-30s median %8.1f us  min %8.1f us  %7.1f GB/s  %.1f%%\n",
+                  v.name.c_str(), med, v.us[0], bytes / med / 1e3, bytes / med / 1e3 / 80.0);
+    }
+    CK(hipFree(in));
+    CK(hipFree(out));
+    CK(hipFree(dt));
+  }
+  return 0;
+}
