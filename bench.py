@@ -61,6 +61,10 @@ def parse():
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal of the "
+                        "multi-rank logic with several ranks on one GPU, see "
+                        "STORB_BENCH_DEVICE)")
     return p.parse_args()
 
 
@@ -120,6 +124,32 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256):
     return {"value": round(reps * nchunks * chunk_bytes / GIB / el, 3), "unit": "GiB/s",
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB pageable "
                     "host chunks -> pinned H2D -> encode -> D2H parity, 2 streams"}
+
+
+def shard_hash_rate(ctx, w, stream, reps=3):
+    """blake3 of every shard of the batch where encode left it (Storb's piece
+    ids, upload.rs:623): data shares + parity shares, device-resident."""
+    dev = w.data.device
+    hd = torch.empty(w.N * w.k * 32, dtype=torch.uint8, device=dev)
+    hp = torch.empty(w.N * (w.n - w.k) * 32, dtype=torch.uint8, device=dev)
+    sp = stream.cuda_stream
+
+    def go():
+        ctx.blake3_batch_dev(w.dptr, w.B, w.N * w.k, w.B, hd.data_ptr(), stream=sp)
+        ctx.blake3_batch_dev(w.pptr, w.B, w.N * (w.n - w.k), w.B, hp.data_ptr(), stream=sp)
+
+    go()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        go()
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = w.N * w.n * w.B
+    return {"value": round(nbytes / (ms * 1e-3) / 1e9, 1), "unit": "GB/s of shard bytes",
+            "ms": round(ms, 4), "shards": w.N * w.n, "shard_bytes": w.B,
+            "what": "blake3 (Storb piece id) of all data+parity shards, batched kernel"}
 
 
 class Workload:
@@ -203,10 +233,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # STORB_BENCH_DEVICE pins every rank to one GPU (multi-rank rehearsal on a
+    # single-GPU box with --dist-backend gloo); by default rank i uses GPU i.
+    local = int(os.environ.get("STORB_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     ctx = _lib.Context(local)
     ctx.set_kernel(_lib.KERNEL_LDS if a.kernel == "lds" else _lib.KERNEL_PERM)
@@ -257,7 +293,8 @@ def main():
     leg_ms = [sum(e[j].elapsed_time(e[j + 1]) for e in ev) / a.steps for j in range(len(legs))]
     units = w.N * w.chunk * len(legs)  # user bytes per step on this rank
     if world > 1:
-        t = torch.tensor([elapsed, float(units)], dtype=torch.float64, device=dev)
+        tdev = dev if a.dist_backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed, float(units)], dtype=torch.float64, device=tdev)
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t[1:].clone()
@@ -322,6 +359,8 @@ def main():
                                                do_decode="decode" in w.legs)
         if not a.no_host_path and a.config == 2:
             out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk)
+        if a.config == 2:
+            out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -135,6 +135,19 @@ int storb_rs_apply_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t rows,
                        const size_t *out_stride, size_t block,
                        uint32_t nstripes, void *hip_stream);
 
+/* ---- shard identity: BLAKE3 (hash mode, 32-byte digest) --------------- */
+/* Storb names every shard by blake3(shard bytes): upload.rs:623,
+ * crates/storb_miner/src/lib.rs:265-283, download.rs:158-161 (crate blake3
+ * 1.8.2, reference Cargo.lock:1099). Host one-shot hash: */
+void storb_blake3(const uint8_t *data, size_t len, uint8_t out[32]);
+/* Device batch: message i = len bytes at d_in + i*stride (i < count); digest
+ * i -> d_out + 32*i (device memory). len <= 16 MiB. Hashes the shards where
+ * the encode kernel left them: data shares of N packed stripes are
+ * (d_data, B, N*k, stride B), parity shares (d_parity, B, N*(n-k), B). */
+int storb_rs_blake3_batch_dev(storb_rs_ctx *ctx, const uint8_t *d_in, size_t len,
+                              uint32_t count, size_t stride, uint8_t *d_out,
+                              void *hip_stream);
+
 /* ---- synthetic input (benchmarks / tests) ----------------------------- */
 /* Object o (o < nobj) at d + o*obj_stride gets obj_len bytes of the
  * little-endian splitmix64 stream seeded with seed_base + o. */

@@ -75,6 +75,9 @@ def _declare(L):
                                      C.POINTER(sz), C.POINTER(vp), C.POINTER(sz), sz,
                                      C.c_uint32, vp]
     L.storb_rs_fill_splitmix_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, C.c_uint64, vp]
+    L.storb_blake3.argtypes = [vp, sz, vp]
+    L.storb_blake3.restype = None
+    L.storb_rs_blake3_batch_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, vp, vp]
     L.storb_rs_set_kernel.argtypes = [vp, C.c_int]
     L.storb_rs_sync.argtypes = [vp]
 
@@ -130,6 +133,14 @@ def get_k_and_m(chunk_size: int) -> tuple[int, int]:
     k, m = C.c_uint64(), C.c_uint64()
     lib().storb_get_k_and_m(chunk_size, C.byref(k), C.byref(m))
     return int(k.value), int(m.value)
+
+
+def blake3(data) -> bytes:
+    """Host BLAKE3 digest (32 bytes) -- Storb's shard identity."""
+    buf = _as_u8(data)
+    out = np.zeros(32, dtype=np.uint8)
+    lib().storb_blake3(buf.ctypes.data if buf.size else None, buf.size, out.ctypes.data)
+    return out.tobytes()
 
 
 def _as_u8(data) -> np.ndarray:
@@ -250,6 +261,12 @@ class Context:
         rc = lib().storb_rs_fill_splitmix_dev(self._h, d, obj_len, nobj, obj_stride,
                                               seed_base, self._s(stream))
         self._check(rc, "storb_rs_fill_splitmix_dev")
+
+    def blake3_batch_dev(self, d_in: int, length: int, count: int, stride: int, d_out: int,
+                         stream: Optional[int] = None):
+        rc = lib().storb_rs_blake3_batch_dev(self._h, d_in, length, count, stride, d_out,
+                                             self._s(stream))
+        self._check(rc, "storb_rs_blake3_batch_dev")
 
     def set_kernel(self, variant: int):
         self._check(lib().storb_rs_set_kernel(self._h, variant), "storb_rs_set_kernel")

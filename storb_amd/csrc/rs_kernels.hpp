@@ -49,6 +49,9 @@ bool vector_ok(const ApplyArgs &a);
 
 hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s);
 
+hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
+                               uint64_t stride, uint8_t *out, hipStream_t s);
+
 hipError_t launch_fill_splitmix(uint8_t *d, uint64_t obj_len, uint32_t nobj,
                                 uint64_t obj_stride, uint64_t seed_base,
                                 hipStream_t s);

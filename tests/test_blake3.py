@@ -1,0 +1,105 @@
+"""BLAKE3 shard identity (Storb: upload.rs:623, miner lib.rs:265-283,
+download.rs:158-161; crate blake3 1.8.2).
+
+Pins: the published BLAKE3 vectors -- hash of the empty input and of "abc",
+and entries of the official test_vectors.json (input byte i = i % 251) --
+against the restated reference (oracle/blake3_ref.py); then the product's host
+hasher and its gfx950 batch kernel against that reference, bit-exact.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle.blake3_ref import blake3 as ref
+from storb_amd import _lib
+
+
+def tv(n):
+    return bytes(i % 251 for i in range(n))
+
+
+PUBLISHED = {
+    # official test_vectors.json, 32-byte hash mode outputs
+    0: "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262",
+    1: "2d3adedff11b61f14c886e35afa036736dcd87a74d27b5c1510225d0f592e213",
+    1023: "10108970eeda3eb932baac1428c7a2163b0e924c9a9e25b35bba72b28f70bd11",
+    1024: "42214739f095a406f3fc83deb889744ac00df831c10daa55189b5d121c855af7",
+    1025: "d00278ae47eb27b34faecf67b4fe263f82d5412916c1ffd97c8cb7fb814b8444",
+}
+
+
+def test_reference_matches_published_vectors():
+    assert ref(b"abc").hex() == "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85"
+    for n, h in PUBLISHED.items():
+        assert ref(tv(n)).hex() == h, n
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 2049, 3072,
+                               3073, 4096, 4097, 5121, 8193, 16384, 31744, 102400])
+def test_host_hasher_matches_reference(n):
+    assert _lib.blake3(tv(n)) == ref(tv(n))
+
+
+def test_host_hasher_random_sizes():
+    rng = random.Random(3)
+    for _ in range(12):
+        n = rng.randrange(0, 200000)
+        d = rng.randbytes(n)
+        assert _lib.blake3(d) == ref(d)
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("length,count,stride,offset", [
+    (0, 3, 16, 0), (1, 5, 16, 0), (64, 4, 64, 0), (1000, 3, 1024, 0), (1024, 4, 1024, 0),
+    (1025, 3, 1040, 0), (4099, 3, 4112, 3), (256 << 10, 6, 256 << 10, 0),
+    (300 * 1024 + 5, 2, 300 * 1024 + 16, 0), (1 << 20, 3, 1 << 20, 0),
+    ((1 << 20) + 17, 2, (1 << 20) + 32, 1), (4 << 20, 2, 4 << 20, 0), (16 << 20, 1, 16 << 20, 0)])
+def test_device_batch_matches_host(ctx, length, count, stride, offset):
+    import torch
+    host = np.frombuffer(np.random.default_rng(length + count).bytes(count * stride + offset + 16),
+                         dtype=np.uint8).copy()
+    d = torch.from_numpy(host).to("cuda:0")
+    out = torch.zeros(count * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.blake3_batch_dev(d.data_ptr() + offset, length, count, stride, out.data_ptr())
+    got = out.cpu().numpy().reshape(count, 32)
+    for i in range(count):
+        msg = host[offset + i * stride: offset + i * stride + length].tobytes()
+        assert got[i].tobytes() == _lib.blake3(msg), (length, i)
+    if length <= 1 << 20:
+        assert got[0].tobytes() == ref(host[offset:offset + length].tobytes())
+
+
+@pytest.mark.gpu
+def test_device_hashes_of_encoded_shards(ctx):
+    """Storb's piece hashes for a batch of RS(4,2) 1 MiB chunks, computed where
+    encode left the shards, equal blake3 of the host-side shards."""
+    import torch
+    from oracle import coracle
+    k, n, L, N = 4, 6, 1 << 20, 8
+    B = L // k
+    data = torch.empty(N * L, dtype=torch.uint8, device="cuda:0")
+    par = torch.empty(N * (n - k) * B, dtype=torch.uint8, device="cuda:0")
+    ctx.fill_splitmix_dev(data.data_ptr(), L, N, L, 0x5709B)
+    ctx.encode_batch_dev(k, n, B, N, data.data_ptr(), par.data_ptr())
+    hd = torch.empty(N * k * 32, dtype=torch.uint8, device="cuda:0")
+    hp = torch.empty(N * (n - k) * 32, dtype=torch.uint8, device="cuda:0")
+    ctx.blake3_batch_dev(data.data_ptr(), B, N * k, B, hd.data_ptr())
+    ctx.blake3_batch_dev(par.data_ptr(), B, N * (n - k), B, hp.data_ptr())
+    hd = hd.cpu().numpy().reshape(N, k, 32)
+    hp = hp.cpu().numpy().reshape(N, n - k, 32)
+    for s in (0, N - 1):
+        shares, _, _ = coracle.encode(k, n, coracle.splitmix_bytes(0x5709B + s, L))
+        for i in range(n):
+            want = _lib.blake3(shares[i].tobytes())
+            got = hd[s, i] if i < k else hp[s, i - k]
+            assert got.tobytes() == want, (s, i)
+
+
+@pytest.mark.gpu
+def test_device_batch_rejects_oversize(ctx):
+    with pytest.raises(_lib.StorbRsError) as e:
+        ctx.blake3_batch_dev(0, (16 << 20) + 1, 1, 0, 0)
+    assert e.value.code == _lib.EINVAL
