@@ -100,6 +100,14 @@ int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
 int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                            const uint8_t *data, size_t chunk_len,
                            uint32_t nchunks, uint8_t *parity_out);
+/* Same, plus every share's blake3 piece id (upload.rs:623) computed on the
+ * GPU where the shares already are: hashes_out + (c*n + i)*32 receives the
+ * digest of share i (data i < k, parity i >= k) of chunk c. Data shares
+ * never travel back over PCIe; only their 32-byte ids do. */
+int storb_rs_encode_chunks_hashed(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                                  const uint8_t *data, size_t chunk_len,
+                                  uint32_t nchunks, uint8_t *parity_out,
+                                  uint8_t *hashes_out);
 
 /* ---- device-resident batched variants -------------------------------- */
 /* Stripe s, data share j lives at d_data + s*data_stride + j*block; parity

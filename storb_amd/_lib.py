@@ -66,6 +66,8 @@ def _declare(L):
     L.storb_rs_decode.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(vp),
                                   C.POINTER(C.c_uint32), C.c_uint32, sz, sz, vp]
     L.storb_rs_encode_chunks.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.c_uint32, vp]
+    L.storb_rs_encode_chunks_hashed.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.c_uint32,
+                                                vp, vp]
     L.storb_rs_encode_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
                                             vp, sz, vp, sz, vp]
     L.storb_rs_decode_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
@@ -224,6 +226,20 @@ class Context:
                                           nchunks, out.ctypes.data)
         self._check(rc, "storb_rs_encode_chunks")
         return out
+
+    def encode_chunks_hashed(self, k: int, n: int, data: np.ndarray, chunk_len: int,
+                             nchunks: int):
+        """(parity [nchunks*(n-k)*B], digests [nchunks, n, 32]) -- piece ids
+        computed on the GPU."""
+        buf = _as_u8(data)
+        assert buf.size >= chunk_len * nchunks
+        B = block_size(k, chunk_len)
+        par = np.empty(max(1, nchunks * (n - k) * B), dtype=np.uint8)
+        hashes = np.empty((nchunks, n, 32), dtype=np.uint8)
+        rc = lib().storb_rs_encode_chunks_hashed(self._h, k, n, buf.ctypes.data, chunk_len,
+                                                 nchunks, par.ctypes.data, hashes.ctypes.data)
+        self._check(rc, "storb_rs_encode_chunks_hashed")
+        return par[:nchunks * (n - k) * B], hashes
 
     # --------------------------------------------------- device buffers
     def encode_batch_dev(self, k: int, n: int, block: int, nstripes: int, d_data: int,

@@ -675,44 +675,60 @@ int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
 // Pipelined batch encode: two pinned in/out buffer pairs and two streams.
 // While the GPU copies and encodes batch i, the host packs batch i+1 and
 // unpacks batch i-1 (hipMemcpyAsync from pinned memory is a true DMA).
-int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
-                           size_t chunk_len, uint32_t nchunks, uint8_t *parity_out) {
+// With hashes_out, the blake3 of every share is computed on the device
+// right after the encode kernel and only the digests come back.
+static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                              const uint8_t *data, size_t chunk_len, uint32_t nchunks,
+                              uint8_t *parity_out, uint8_t *hashes_out) {
   if (!ctx) return STORB_RS_EINVAL;
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
   if (chunk_len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
   const uint32_t p = n - k;
-  if (p == 0 || nchunks == 0) return STORB_RS_OK;
-  if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  if (nchunks == 0) return STORB_RS_OK;
+  if (p > 0 && !parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
   const size_t B = (chunk_len + k - 1) / k;
+  if (hashes_out && B > 16ull * 1024 * 1024)
+    return fail(ctx, STORB_RS_EINVAL, "blake3: share larger than 16 MiB");
   const size_t S = round_up(B, kAlign);
   const bool packed = (S == B) && (B * k == chunk_len);
   // ~64 MiB of input per batch keeps both DMA directions busy.
   const size_t per = static_cast<size_t>(k) * S;
   uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
   batch = std::min(batch, nchunks);
+  const size_t hash_bytes = hashes_out ? static_cast<size_t>(batch) * n * 32 : 0;
   DeviceGuard g(ctx->device);
   for (int b = 0; b < 2; b++) {
     HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
-    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch));
-    HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch));
+    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch + hash_bytes));
+    HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
   }
   const std::vector<uint8_t> &enc = cached_enc(k, n);
-  const Tables *t = nullptr;
-  int rc = get_tables(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, ctx->pipe[0], &t);
-  if (rc) return rc;
   const uint32_t nb = (nchunks + batch - 1) / batch;
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;
     const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
-    if (S == B) {
-      std::memcpy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
-                  static_cast<size_t>(cn) * p * B);
-    } else {
-      for (uint32_t c = 0; c < cn; c++)
-        for (uint32_t i = 0; i < p; i++)
-          std::memcpy(parity_out + ((static_cast<size_t>(c0) + c) * p + i) * B,
-                      ctx->pipe_out[b].p + (static_cast<size_t>(c) * p + i) * S, B);
+    if (p > 0) {
+      if (S == B) {
+        std::memcpy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
+                    static_cast<size_t>(cn) * p * B);
+      } else {
+        for (uint32_t c = 0; c < cn; c++)
+          for (uint32_t i = 0; i < p; i++)
+            std::memcpy(parity_out + ((static_cast<size_t>(c0) + c) * p + i) * B,
+                        ctx->pipe_out[b].p + (static_cast<size_t>(c) * p + i) * S, B);
+      }
+    }
+    if (hashes_out) {
+      // device order: [c][j] data digests, then [c][i] parity digests
+      const uint8_t *hd = ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch;
+      const uint8_t *hp = hd + static_cast<size_t>(cn) * k * 32;
+      for (uint32_t c = 0; c < cn; c++) {
+        uint8_t *o = hashes_out + (static_cast<size_t>(c0) + c) * n * 32;
+        std::memcpy(o, hd + static_cast<size_t>(c) * k * 32, static_cast<size_t>(k) * 32);
+        std::memcpy(o + static_cast<size_t>(k) * 32, hp + static_cast<size_t>(c) * p * 32,
+                    static_cast<size_t>(p) * 32);
+      }
     }
   };
   for (uint32_t bi = 0; bi < nb; bi++) {
@@ -740,23 +756,49 @@ int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint
     }
     uint8_t *dd = ctx->pipe_dev[b].p;
     uint8_t *dp = dd + per * batch;
+    uint8_t *dh = dp + static_cast<size_t>(p) * S * batch;  // digests (if any)
     HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
-    std::vector<const uint8_t *> in(k);
-    std::vector<uint8_t *> out(p);
-    std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
-    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
-    for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
-    rc = apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(), ins.data(),
-               out.data(), outs.data(), S, cn, s);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dp, static_cast<size_t>(p) * S * cn,
-                                hipMemcpyDeviceToHost, s));
+    if (p > 0) {
+      std::vector<const uint8_t *> in(k);
+      std::vector<uint8_t *> out(p);
+      std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
+      for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
+      for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
+      const int rc = apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(),
+                           ins.data(), out.data(), outs.data(), S, cn, s);
+      if (rc) return rc;
+    }
+    size_t back = static_cast<size_t>(p) * S * cn;
+    if (hashes_out) {
+      // shares are pitched S apart across the whole batch: one launch each
+      HIP_TRY(ctx, launch_blake3_batch(dd, B, cn * k, S, dh, s));
+      if (p > 0)
+        HIP_TRY(ctx, launch_blake3_batch(dp, B, cn * p, S, dh + static_cast<size_t>(cn) * k * 32,
+                                         s));
+    }
+    if (back)
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dp, back, hipMemcpyDeviceToHost, s));
+    if (hashes_out)
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch, dh,
+                                  static_cast<size_t>(cn) * n * 32, hipMemcpyDeviceToHost, s));
   }
   for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[bi & 1]));
     unpack(bi);
   }
   return STORB_RS_OK;
+}
+
+int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                           size_t chunk_len, uint32_t nchunks, uint8_t *parity_out) {
+  return encode_chunks_impl(ctx, k, n, data, chunk_len, nchunks, parity_out, nullptr);
+}
+
+int storb_rs_encode_chunks_hashed(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                                  const uint8_t *data, size_t chunk_len, uint32_t nchunks,
+                                  uint8_t *parity_out, uint8_t *hashes_out) {
+  if (!hashes_out) return STORB_RS_EINVAL;
+  return encode_chunks_impl(ctx, k, n, data, chunk_len, nchunks, parity_out, hashes_out);
 }
 
 }  // extern "C"

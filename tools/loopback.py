@@ -1,0 +1,303 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: loopback upload -> store -> retrieve -> reconstruct.
+
+One validator (this process) and N miner processes on 127.0.0.1 speak
+Storb's formats (storb_amd/wire.py). The object is chunked as the reference
+does (upload.rs:209,333-383: chunk = piece_length(object len)); each chunk is
+RS-encoded on the GPU with every shard's blake3 id computed on the device
+(storb_rs_encode_chunks_hashed: pinned H2D of data, D2H of parity and ids
+only); pieces go to miners over the store framing and each miner's ack must
+equal the id; one miner is killed (seeded); download gathers k+1 pieces per
+chunk in piece_idx order (download.rs:336-451), verifies blake3, and
+reconstructs with decode_chunk's rule (sort, first k) on the GPU
+(storb_rs_decode). The reference itself cannot run this offline (live
+chain, network-fetched crsqlite, >100-chunk channel hang,
+download.rs:26,500) -- see SURVEY.md fact 9.
+
+usage: python tools/loopback.py [--size BYTES] [--miners N] [--json]
+       python tools/loopback.py miner --store-port P --http-port Q --dir D
+"""
+from __future__ import annotations
+
+import argparse
+import http.client
+import http.server
+import json
+import os
+import random
+import shutil
+import socket
+import socketserver
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from urllib.parse import parse_qs, urlparse
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from storb_amd import _lib, partition, wire  # noqa: E402
+
+GIB = float(1 << 30)
+HANDSHAKE = bytes(96)  # opaque HandshakePayload bytes (auth out of scope)
+
+
+# ------------------------------------------------------------------ miner
+def miner_main(a):
+    store = wire.ObjectStore(a.dir)
+
+    class StoreHandler(socketserver.BaseRequestHandler):
+        def handle(self):
+            sock = self.request
+            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            while True:
+                frame = wire.read_store_frame(sock)
+                if frame is None:
+                    return
+                _, piece = frame
+                h = _lib.blake3(piece)  # lib.rs:265
+                store.write(h.hex(), piece)
+                sock.sendall(h + b"\n")
+
+    class PieceHandler(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def do_GET(self):
+            u = urlparse(self.path)
+            q = parse_qs(u.query)
+            try:
+                if u.path != "/piece" or "handshake" not in q:
+                    raise ValueError
+                hexhash = q["piecehash"][0]
+                body = wire.serialise_piece_response(bytes.fromhex(hexhash),
+                                                     store.read(hexhash))
+                code = 200
+            except Exception:
+                body, code = b"error", 500
+            self.send_response(code)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *args):
+            pass
+
+    class TS(socketserver.ThreadingMixIn, socketserver.TCPServer):
+        daemon_threads = True
+        allow_reuse_address = True
+
+    class HS(http.server.ThreadingHTTPServer):
+        daemon_threads = True
+
+    s1 = TS(("127.0.0.1", a.store_port), StoreHandler)
+    s2 = HS(("127.0.0.1", a.http_port), PieceHandler)
+    threading.Thread(target=s1.serve_forever, daemon=True).start()
+    threading.Thread(target=s2.serve_forever, daemon=True).start()
+    print("ready", flush=True)
+    while True:
+        time.sleep(3600)
+
+
+# -------------------------------------------------------------- validator
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def splitmix_bytes(seed: int, n: int) -> np.ndarray:
+    i = np.arange(1, -(-n // 8) + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + i * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return z.view(np.uint8)[:n]
+
+
+def run(a):
+    tmp = tempfile.mkdtemp(prefix="storb_loop_")
+    miners = []
+    for m in range(a.miners):
+        sp, hp = free_port(), free_port()
+        proc = subprocess.Popen([sys.executable, os.path.abspath(__file__), "miner",
+                                 "--store-port", str(sp), "--http-port", str(hp),
+                                 "--dir", os.path.join(tmp, f"miner{m}")],
+                                stdout=subprocess.PIPE, text=True)
+        miners.append({"proc": proc, "store": sp, "http": hp})
+    for m in miners:
+        if m["proc"].stdout.readline().strip() != "ready":
+            raise SystemExit("miner failed to start")
+    try:
+        return _run(a, miners)
+    finally:
+        for m in miners:
+            if m["proc"].poll() is None:
+                m["proc"].kill()
+            m["proc"].wait()
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _run(a, miners):
+    M = len(miners)
+    ctx = _lib.Context(-1)
+    obj = splitmix_bytes(0x5709B + a.seed, a.size)
+    chunk_size = _lib.piece_length(a.size)
+    chunks = partition.chunks_of(a.size, chunk_size)
+    metas = []  # per chunk: k, m, B, padlen, piece hashes, miner per piece
+
+    # ---- upload: GPU encode + GPU piece ids, then the store framing
+    t0 = time.perf_counter()
+    groups = {}
+    for ci, (off, ln) in enumerate(chunks):
+        groups.setdefault(ln, []).append(ci)
+    parity_of, hashes_of = {}, {}
+    for ln, idxs in groups.items():
+        k, n = _lib.get_k_and_m(ln)
+        lo = idxs[0]
+        assert idxs == list(range(lo, lo + len(idxs)))
+        par, hashes = ctx.encode_chunks_hashed(k, n, obj[lo * chunk_size:lo * chunk_size +
+                                                          len(idxs) * ln], ln, len(idxs))
+        B = _lib.block_size(k, ln)
+        par = par.reshape(len(idxs), n - k, B)
+        for j, ci in enumerate(idxs):
+            parity_of[ci], hashes_of[ci] = par[j], hashes[j]
+    t_encode = time.perf_counter() - t0
+
+    per_miner = [[] for _ in range(M)]
+    for ci, (off, ln) in enumerate(chunks):
+        k, n = _lib.get_k_and_m(ln)
+        B = _lib.block_size(k, ln)
+        padded = obj[off:off + ln]
+        if B * k != ln:
+            padded = np.concatenate([padded, np.zeros(B * k - ln, dtype=np.uint8)])
+        metas.append({"k": k, "m": n, "B": B, "padlen": B * k - ln, "off": off, "len": ln,
+                      "hashes": [hashes_of[ci][i].tobytes() for i in range(n)],
+                      "miner": [(ci * n + i) % M for i in range(n)]})
+        for i in range(n):
+            piece = padded[i * B:(i + 1) * B] if i < k else parity_of[ci][i - k]
+            per_miner[(ci * n + i) % M].append((ci, i, piece))
+
+    def upload(m):
+        s = socket.create_connection(("127.0.0.1", miners[m]["store"]))
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        bad = 0
+        for ci, i, piece in per_miner[m]:
+            ack = wire.send_piece(s, HANDSHAKE, piece)
+            bad += ack != metas[ci]["hashes"][i]
+        s.close()
+        return bad
+
+    with ThreadPoolExecutor(M) as ex:
+        ack_mismatch = sum(ex.map(upload, range(M)))
+    t_upload = time.perf_counter() - t0
+    if ack_mismatch:
+        raise SystemExit(f"{ack_mismatch} miner acks differ from the GPU piece ids")
+
+    # ---- a seeded miner failure
+    dead = random.Random(a.kill_seed).randrange(M)
+    miners[dead]["proc"].kill()
+    miners[dead]["proc"].wait()
+
+    # ---- download: > k unique pieces per chunk, blake3-verified, then decode
+    t1 = time.perf_counter()
+    tls = threading.local()
+
+    def fetch(m, hexhash):
+        conns = getattr(tls, "conns", None)
+        if conns is None:
+            conns = tls.conns = {}
+        c = conns.get(m)
+        if c is None:
+            c = conns[m] = http.client.HTTPConnection("127.0.0.1", miners[m]["http"], timeout=10)
+        c.request("GET", f"/piece?piecehash={hexhash}&handshake={HANDSHAKE.hex()}")
+        r = c.getresponse()
+        body = r.read()
+        if r.status != 200:
+            raise IOError("miner error")
+        return body
+
+    def gather(ci):
+        meta = metas[ci]
+        got = {}
+        for i in range(meta["m"]):  # get_pieces_by_chunk: ORDER BY piece_idx
+            if len(got) > meta["k"]:
+                break
+            h = meta["hashes"][i]
+            try:
+                body = fetch(meta["miner"][i], h.hex())
+                got[i] = wire.deserialise_piece_response(body, h)  # blake3 check
+            except (OSError, ValueError, http.client.HTTPException):
+                if hasattr(tls, "conns"):
+                    tls.conns.pop(meta["miner"][i], None)
+        return ci, got
+
+    with ThreadPoolExecutor(16) as ex:
+        gathered = dict(ex.map(gather, range(len(chunks))))
+    t_fetch = time.perf_counter() - t1
+
+    out = np.empty(a.size, dtype=np.uint8)
+    needed_parity = 0
+    t2 = time.perf_counter()
+    for ci, meta in enumerate(metas):
+        got = gathered[ci]
+        if len(got) < meta["k"]:
+            raise SystemExit(f"chunk {ci}: not enough pieces ({len(got)} < {meta['k']})")
+        idx = sorted(got)[:meta["k"]]  # decode_chunk: sort, first k
+        needed_parity += any(i >= meta["k"] for i in idx)
+        rec = ctx.decode(meta["k"], meta["m"], [got[i] for i in idx], idx, meta["B"],
+                         meta["padlen"])
+        out[meta["off"]:meta["off"] + meta["len"]] = np.frombuffer(rec, dtype=np.uint8)
+    t_decode = time.perf_counter() - t2
+    t_download = time.perf_counter() - t1
+    ok = bool(np.array_equal(out, obj))
+    nshards = sum(m["m"] for m in metas)
+    res = {
+        "config": "BASELINE 5 loopback (validator + miners on 127.0.0.1)",
+        "object_bytes": a.size, "chunks": len(chunks), "chunk_bytes": chunk_size,
+        "k_m": sorted({(m["k"], m["m"]) for m in metas}), "shards": nshards,
+        "shard_bytes_total": sum(m["m"] * m["B"] for m in metas), "miners": M,
+        "killed_miner": dead, "chunks_decoded_through_parity": needed_parity,
+        "bit_exact": ok, "ack_mismatch": ack_mismatch,
+        "t_encode_s": round(t_encode, 4), "t_upload_s": round(t_upload, 4),
+        "t_fetch_s": round(t_fetch, 4), "t_decode_s": round(t_decode, 4),
+        "t_download_s": round(t_download, 4),
+        "encode_GiBps": round(a.size / GIB / t_encode, 3),
+        "upload_GiBps": round(a.size / GIB / t_upload, 3),
+        "download_GiBps": round(a.size / GIB / t_download, 3),
+        "end_to_end_GiBps": round(a.size / GIB / (t_upload + t_download), 3),
+        "device": ctx.device,
+    }
+    return res
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "miner":
+        p = argparse.ArgumentParser()
+        p.add_argument("role")
+        p.add_argument("--store-port", type=int, required=True)
+        p.add_argument("--http-port", type=int, required=True)
+        p.add_argument("--dir", required=True)
+        miner_main(p.parse_args())
+        return
+    p = argparse.ArgumentParser()
+    p.add_argument("--size", type=int, default=1 << 30)
+    p.add_argument("--miners", type=int, default=8)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--kill-seed", type=int, default=7)
+    a = p.parse_args()
+    res = run(a)
+    print(json.dumps(res), flush=True)
+    if not res["bit_exact"]:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
