@@ -24,55 +24,148 @@ namespace {
 constexpr int kB3Threads = 256;
 typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void load_block(uint32_t *m, const uint8_t *p, uint32_t bl,
-                                           bool aligned16) {
-  if (bl == b3::kBlockLen && aligned16) {
-    const u32x4b *q = reinterpret_cast<const u32x4b *>(p);
+// One out-of-line copy of the 7-round compression (~700 instructions): the
+// chunk, parent and root paths all call it, so the kernel's code stays
+// inside the instruction cache (inlined it was ~6k instructions).
+// Arguments are scalars and the result a small struct so the call passes
+// everything in VGPRs (array pointers would force the arrays to scratch).
+struct CV8 {
+  uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+};
+
+__device__ __forceinline__ CV8 compress_dev(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                         uint32_t c4, uint32_t c5, uint32_t c6, uint32_t c7,
+                                         uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3,
+                                         uint32_t m4, uint32_t m5, uint32_t m6, uint32_t m7,
+                                         uint32_t m8, uint32_t m9, uint32_t m10, uint32_t m11,
+                                         uint32_t m12, uint32_t m13, uint32_t m14, uint32_t m15,
+                                         uint32_t ctr_lo, uint32_t ctr_hi, uint32_t block_len,
+                                         uint32_t flags) {
+  uint32_t cv[8] = {c0, c1, c2, c3, c4, c5, c6, c7};
+  const uint32_t m[16] = {m0, m1, m2, m3, m4, m5, m6, m7, m8, m9, m10, m11, m12, m13, m14, m15};
+  b3::compress_cv(cv, m, (static_cast<uint64_t>(ctr_hi) << 32) | ctr_lo, block_len, flags);
+  return CV8{cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7]};
+}
+
+__device__ __forceinline__ void compress_call(uint32_t *cv, const uint32_t *m, uint64_t counter,
+                                              uint32_t block_len, uint32_t flags) {
+  const CV8 r = compress_dev(cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7], m[0], m[1],
+                             m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[9], m[10], m[11], m[12],
+                             m[13], m[14], m[15], static_cast<uint32_t>(counter),
+                             static_cast<uint32_t>(counter >> 32), block_len, flags);
+  cv[0] = r.w0;
+  cv[1] = r.w1;
+  cv[2] = r.w2;
+  cv[3] = r.w3;
+  cv[4] = r.w4;
+  cv[5] = r.w5;
+  cv[6] = r.w6;
+  cv[7] = r.w7;
+}
+
+__device__ __forceinline__ void parent_dev(uint32_t *out, const uint32_t *l, const uint32_t *r,
+                                           uint32_t extra_flags) {
+  uint32_t m[16];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const u32x4b v = __builtin_nontemporal_load(q + i);
-      m[4 * i] = v[0];
-      m[4 * i + 1] = v[1];
-      m[4 * i + 2] = v[2];
-      m[4 * i + 3] = v[3];
+  for (int i = 0; i < 8; i++) {
+    m[i] = l[i];
+    m[i + 8] = r[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = b3::iv(i);
+  compress_call(out, m, 0, b3::kBlockLen, b3::kParent | extra_flags);
+}
+
+// Partial or unaligned block: byte loads, zero padded (rare path).
+__device__ __forceinline__ void load_block_bytes(uint32_t *m, const uint8_t *p, uint32_t bl) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    uint32_t w = 0;
+    for (int b = 0; b < 4; b++) {
+      const uint32_t o = 4 * i + b;
+      if (o < bl) w |= static_cast<uint32_t>(p[o]) << (8 * b);
     }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const uint32_t o = 4 * i + b;
-        if (o < bl) w |= static_cast<uint32_t>(p[o]) << (8 * b);
-      }
-      m[i] = w;
-    }
+    m[i] = w;
   }
 }
 
+__device__ __forceinline__ void load_block16(u32x4b *v, const uint8_t *p) {
+  const u32x4b *q = reinterpret_cast<const u32x4b *>(p);
+#pragma unroll
+  for (int i = 0; i < 4; i++) v[i] = q[i];  // cached: the 4 loads share lines
+}
+
+// Two full, 16-B aligned chunks hashed together: the two compressions per
+// block step are independent, which doubles the ILP of BLAKE3's serial G
+// chains (one chunk per lane measured ~65 % SQ_WAIT_INST_ANY).
+__device__ void chunk_cv_pair(uint32_t *cva, uint32_t *cvb, const uint8_t *pa, uint64_t idx) {
+  const uint8_t *pb = pa + b3::kChunkLen;
+#pragma unroll
+  for (int i = 0; i < 8; i++) cva[i] = cvb[i] = b3::iv(i);
+  u32x4b na[4], nb[4];
+  load_block16(na, pa);
+  load_block16(nb, pb);
+  for (uint32_t b = 0; b < b3::kChunkLen / b3::kBlockLen; b++) {
+    uint32_t ma[16], mb[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        ma[4 * i + e] = na[i][e];
+        mb[4 * i + e] = nb[i][e];
+      }
+    if (b + 1 < b3::kChunkLen / b3::kBlockLen) {
+      load_block16(na, pa + (b + 1) * b3::kBlockLen);
+      load_block16(nb, pb + (b + 1) * b3::kBlockLen);
+    }
+    const uint32_t flags = (b == 0 ? b3::kChunkStart : 0) | (b == 15 ? b3::kChunkEnd : 0);
+    b3::compress_cv(cva, ma, idx, b3::kBlockLen, flags);
+    b3::compress_cv(cvb, mb, idx + 1, b3::kBlockLen, flags);
+  }
+}
+
+// Chunk chaining value; full aligned blocks are software-pipelined: the next
+// block's four dwordx4 loads are in flight while the current block is
+// compressed.
 __device__ void chunk_cv_dev(uint32_t *cv, const uint8_t *p, uint32_t len, uint64_t idx,
                              uint32_t root_flag, bool aligned16) {
   const uint32_t nb = len == 0 ? 1 : (len + b3::kBlockLen - 1) / b3::kBlockLen;
+  const uint32_t nfull = aligned16 ? len / b3::kBlockLen : 0;  // fast-path blocks
 #pragma unroll
   for (int i = 0; i < 8; i++) cv[i] = b3::iv(i);
+  u32x4b nxt[4];
+  if (nfull > 0) load_block16(nxt, p);
   for (uint32_t b = 0; b < nb; b++) {
     const uint32_t off = b * b3::kBlockLen;
     const uint32_t bl = len - off < b3::kBlockLen ? len - off : b3::kBlockLen;
     uint32_t m[16];
-    load_block(m, p + off, bl, aligned16);
+    if (b < nfull) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        m[4 * i] = nxt[i][0];
+        m[4 * i + 1] = nxt[i][1];
+        m[4 * i + 2] = nxt[i][2];
+        m[4 * i + 3] = nxt[i][3];
+      }
+      if (b + 1 < nfull) load_block16(nxt, p + off + b3::kBlockLen);
+    } else {
+      load_block_bytes(m, p + off, bl);
+    }
     const uint32_t flags =
         (b == 0 ? b3::kChunkStart : 0) | (b + 1 == nb ? b3::kChunkEnd | root_flag : 0);
-    b3::compress_cv(cv, m, idx, bl, flags);
+    compress_call(cv, m, idx, bl, flags);
   }
 }
 
-__device__ __forceinline__ void put(uint32_t *base, int slot, int lane, const uint32_t *cv) {
+__device__ __forceinline__ void put(uint32_t *base, int slot, int lane, const uint32_t *cv,
+                                    int T) {
 #pragma unroll
-  for (int w = 0; w < 8; w++) base[(slot * 8 + w) * kB3Threads + lane] = cv[w];
+  for (int w = 0; w < 8; w++) base[(slot * 8 + w) * T + lane] = cv[w];
 }
-__device__ __forceinline__ void get(const uint32_t *base, int slot, int lane, uint32_t *cv) {
+__device__ __forceinline__ void get(const uint32_t *base, int slot, int lane, uint32_t *cv,
+                                    int T) {
 #pragma unroll
-  for (int w = 0; w < 8; w++) cv[w] = base[(slot * 8 + w) * kB3Threads + lane];
+  for (int w = 0; w < 8; w++) cv[w] = base[(slot * 8 + w) * T + lane];
 }
 
 __device__ __forceinline__ void store_hash(uint8_t *o, const uint32_t *cv) {
@@ -99,47 +192,62 @@ __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
     }
     return;
   }
-  uint32_t *stack = lds3;                                  // [depth][8][256]
-  uint32_t *nodes = lds3 + depth * 8 * kB3Threads;         // [2][8][256]
+  const int T = blockDim.x;
+  uint32_t *stack = lds3;                          // [depth][8][T]
+  uint32_t *nodes = lds3 + depth * 8 * T;          // [2][8][T]
   const uint64_t q = 1ull << q_log2;
   const uint64_t c0 = static_cast<uint64_t>(lane) * q;
   const uint64_t c1 = c0 + q < n ? c0 + q : n;
   uint32_t cv[8], left[8];
   int sp = 0;
-  for (uint64_t c = c0; c < c1; c++) {
-    const uint64_t off = c * b3::kChunkLen;
-    const uint32_t clen =
-        static_cast<uint32_t>(len - off < b3::kChunkLen ? len - off : b3::kChunkLen);
-    chunk_cv_dev(cv, p + off, clen, c, 0, aligned16);
-    for (uint64_t t = c - c0 + 1; (t & 1) == 0; t >>= 1) {  // complete subtrees merge
-      get(stack, --sp, lane, left);
-      b3::parent_cv(cv, left, cv, 0);
+  auto push = [&](uint64_t c) {  // merge complete subtrees, then push
+    for (uint64_t t = c - c0 + 1; (t & 1) == 0; t >>= 1) {
+      get(stack, --sp, lane, left, T);
+      parent_dev(cv, left, cv, 0);
     }
-    put(stack, sp++, lane, cv);
+    put(stack, sp++, lane, cv, T);
+  };
+  for (uint64_t c = c0; c < c1;) {
+    if (aligned16 && c + 2 <= c1 && (c + 2) * b3::kChunkLen <= len) {
+      uint32_t cvb[8];
+      chunk_cv_pair(cv, cvb, p + c * b3::kChunkLen, c);
+      push(c);
+#pragma unroll
+      for (int i = 0; i < 8; i++) cv[i] = cvb[i];
+      push(c + 1);
+      c += 2;
+    } else {
+      const uint64_t off = c * b3::kChunkLen;
+      const uint32_t clen =
+          static_cast<uint32_t>(len - off < b3::kChunkLen ? len - off : b3::kChunkLen);
+      chunk_cv_dev(cv, p + off, clen, c, 0, aligned16);
+      push(c);
+      c += 1;
+    }
   }
   if (c1 > c0) {  // a partial (last) group folds right to left
-    get(stack, --sp, lane, cv);
+    get(stack, --sp, lane, cv, T);
     while (sp > 0) {
-      get(stack, --sp, lane, left);
-      b3::parent_cv(cv, left, cv, 0);
+      get(stack, --sp, lane, left, T);
+      parent_dev(cv, left, cv, 0);
     }
-    put(nodes, 0, lane, cv);
+    put(nodes, 0, lane, cv, T);
   }
   __syncthreads();
   uint32_t cnt = static_cast<uint32_t>((n + q - 1) / q);  // >= 2 by the choice of q
   int cur = 0;
   while (cnt > 2) {
     const uint32_t half = cnt / 2;
-    uint32_t *src = nodes + cur * 8 * kB3Threads, *dst = nodes + (cur ^ 1) * 8 * kB3Threads;
+    uint32_t *src = nodes + cur * 8 * T, *dst = nodes + (cur ^ 1) * 8 * T;
     if (static_cast<uint32_t>(lane) < half) {
       uint32_t r[8];
-      get(src, 0, 2 * lane, left);
-      get(src, 0, 2 * lane + 1, r);
-      b3::parent_cv(cv, left, r, 0);
-      put(dst, 0, lane, cv);
+      get(src, 0, 2 * lane, left, T);
+      get(src, 0, 2 * lane + 1, r, T);
+      parent_dev(cv, left, r, 0);
+      put(dst, 0, lane, cv, T);
     } else if ((cnt & 1) && static_cast<uint32_t>(lane) == half) {
-      get(src, 0, cnt - 1, cv);
-      put(dst, 0, lane, cv);
+      get(src, 0, cnt - 1, cv, T);
+      put(dst, 0, lane, cv, T);
     }
     __syncthreads();
     cur ^= 1;
@@ -147,10 +255,10 @@ __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
   }
   if (lane == 0) {
     uint32_t r[8];
-    const uint32_t *src = nodes + cur * 8 * kB3Threads;
-    get(src, 0, 0, left);
-    get(src, 0, 1, r);
-    b3::parent_cv(cv, left, r, b3::kRoot);
+    const uint32_t *src = nodes + cur * 8 * T;
+    get(src, 0, 0, left, T);
+    get(src, 0, 1, r, T);
+    parent_dev(cv, left, r, b3::kRoot);
     store_hash(o, cv);
   }
 }
@@ -165,12 +273,16 @@ hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
   if (count == 0) return hipSuccess;
   if (len > kB3MaxLen) return hipErrorInvalidValue;
   const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
+  // Threads per shard: enough lanes that each owns >= 2 chunks (pairs are
+  // hashed interleaved), between one and four waves.
+  int T = kB3Threads;
+  while (T > 64 && static_cast<uint64_t>(T) * 2 > n) T >>= 1;
   uint32_t q_log2 = 0;
-  while ((static_cast<uint64_t>(kB3Threads) << q_log2) < n) q_log2++;
+  while ((static_cast<uint64_t>(T) << q_log2) < n) q_log2++;
   const uint32_t depth = q_log2 + 1;
-  const size_t lds = (static_cast<size_t>(depth) + 2) * 8 * kB3Threads * sizeof(uint32_t);
-  hipLaunchKernelGGL(blake3_batch_kernel, dim3(count), dim3(kB3Threads), lds, s, in, len,
-                     stride, out, q_log2, depth);
+  const size_t lds = (static_cast<size_t>(depth) + 2) * 8 * T * sizeof(uint32_t);
+  hipLaunchKernelGGL(blake3_batch_kernel, dim3(count), dim3(T), lds, s, in, len, stride, out,
+                     q_log2, depth);
   return hipGetLastError();
 }
 
