@@ -111,6 +111,52 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
     }
 
 
+def cpu_baseline_threads(k, n, chunk_bytes, erased, threads=16, nchunks=96):
+    """The same CPU path on `threads` host cores over independent chunks
+    ("nproc threads on independent chunks"; 16 = this box's
+    CPU share per GPU). Encode + decode round trips, bit-exact checked."""
+    from oracle import coracle  # test infrastructure: the baseline, never the product
+
+    data = np.concatenate([coracle.splitmix_bytes(SEED_BASE + i, chunk_bytes)
+                           for i in range(nchunks)])
+    t0 = time.perf_counter()
+    bad = coracle.roundtrip_many(k, n, data, chunk_bytes, nchunks, sorted(erased), threads)
+    el = time.perf_counter() - t0
+    if bad:
+        raise SystemExit("threaded CPU baseline round trip failed")
+    return {"value": round(2 * nchunks * chunk_bytes / GIB / el, 4), "unit": "GiB/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{nchunks} x encode+decode of {chunk_bytes >> 10} KiB chunks, "
+                      f"{threads} threads, {el:.2f} s"}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def copy_ceiling(dev, stream, nbytes=1 << 30, reps=5):
+    """Measured device-to-device copy rate (read + write bytes / time), the
+    practical HBM ceiling SURVEY 8(d) asks to report beside the 8 TB/s spec."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    with torch.cuda.stream(stream):
+        src.random_(0, 256)
+        dst.copy_(src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            dst.copy_(src)
+        e1.record(stream)
+    stream.synchronize()
+    return round(2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+
+
 def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256):
     """PCIe-inclusive encode: host bytes in, parity out (pinned pipeline)."""
     host = np.frombuffer(np.random.default_rng(7).bytes(nchunks * chunk_bytes),
@@ -349,14 +395,20 @@ def main():
                       f"{(w.n - w.k) if 'encode' in w.legs else len(w.erased)}> (all launches)",
             "leg_ms": {leg: round(ms, 4) for leg, ms in zip(w.legs, leg_ms)},
             "alg_bytes_per_launch": alg,
+            "copy_ceiling_gbs": None,
         },
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
+        out["roofline"]["copy_ceiling_gbs"] = copy_ceiling(dev, stream)
         if a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.erased), a.cpu_seconds,
                                                do_encode="encode" in w.legs,
                                                do_decode="decode" in w.legs)
+            out["cpu_baseline"]["cpu_model"] = cpu_model()
+            if a.config == 2:
+                out["cpu_baseline_threads"] = cpu_baseline_threads(w.k, w.n, w.chunk,
+                                                                   set(w.erased))
         if not a.no_host_path and a.config == 2:
             out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk)
         if a.config == 2:

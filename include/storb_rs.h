@@ -93,6 +93,13 @@ int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                     uint32_t nshares, size_t block, size_t padlen,
                     uint8_t *out);
 
+/* Host-in/host-out repair of one stripe: shares[i] (block bytes) is share
+ * share_idx[i]; share targets[r] is written to out[r] (block bytes). */
+int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                    const uint8_t *const *shares, const uint32_t *share_idx,
+                    uint32_t nshares, size_t block, const uint32_t *targets,
+                    uint32_t ntargets, uint8_t *const *out);
+
 /* Pipelined host batch: nchunks equal-length chunks laid out back to back
  * in host memory (chunk c at data + c*chunk_len). Parity of chunk c, share
  * p lands at parity_out + (c*(n-k) + p)*B. Uses pinned staging and
@@ -133,6 +140,20 @@ int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                               const uint8_t *d_data, size_t data_stride,
                               const uint8_t *d_parity, size_t parity_stride,
                               uint8_t *d_out, size_t out_stride,
+                              void *hip_stream);
+/* Decode-based repair. Storb's repair today re-fetches a
+ * lost piece from another replica (crates/storb_validator/src/repair.rs:
+ * 44-277); with RS it can instead regenerate any share row -- data or
+ * parity -- from the first k surviving shares by index (the same survivor
+ * rule as decode_chunk, piece.rs:368-381). Layout as decode_batch_dev; the
+ * ntargets shares in targets[] are written in place into their own region.
+ * EINVAL if a target is >= n, repeated, or one of the k shares read. */
+int storb_rs_repair_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                              size_t block, uint32_t nstripes,
+                              const uint32_t *share_idx, uint32_t nshares,
+                              const uint32_t *targets, uint32_t ntargets,
+                              uint8_t *d_data, size_t data_stride,
+                              uint8_t *d_parity, size_t parity_stride,
                               void *hip_stream);
 /* The primitive under both: out_r = XOR_j coef[r*k + j] * in_j over GF(2^8)
  * for r < rows, for every stripe (shard s of slot j at d_in[j] +

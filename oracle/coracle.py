@@ -50,6 +50,8 @@ def lib():
         L.zo_splitmix_fill.argtypes = [C.c_uint64, C.c_void_p, C.c_size_t]
         L.zo_encode_many.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_size_t, C.c_uint,
                                      C.c_void_p, C.c_int]
+        L.zo_roundtrip_many.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_size_t, C.c_uint,
+                                        C.POINTER(C.c_uint), C.c_uint, C.c_int]
         _lib = L
     return _lib
 
@@ -117,3 +119,11 @@ def splitmix_bytes(seed: int, length: int) -> np.ndarray:
     out = np.zeros(length, dtype=np.uint8)
     lib().zo_splitmix_fill(seed, _ptr(out), length)
     return out
+
+
+def roundtrip_many(k: int, n: int, data: np.ndarray, chunk_len: int, nchunks: int,
+                   erased, threads: int) -> int:
+    """Threaded encode+decode round trips; returns the number of failures."""
+    er = (C.c_uint * max(1, len(erased)))(*erased)
+    return int(lib().zo_roundtrip_many(k, n, _ptr(data), chunk_len, nchunks, er, len(erased),
+                                       threads))

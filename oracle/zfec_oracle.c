@@ -419,3 +419,71 @@ int zo_encode_many(unsigned k, unsigned n, const uint8_t *data, size_t len,
   free(jobs);
   return 0;
 }
+
+/* ----------------------------------------------- threaded round trips */
+typedef struct {
+  unsigned k, n, first, last, nerased;
+  const unsigned *erased;
+  const uint8_t *data;
+  size_t len;
+  int bad;
+} rt_job;
+
+static void *rt_worker(void *arg) {
+  rt_job *j = (rt_job *)arg;
+  size_t B = (j->len + j->k - 1) / j->k;
+  uint8_t *shares = malloc((size_t)j->n * B);
+  uint8_t *out = malloc(j->len);
+  const uint8_t **sv = malloc(sizeof(uint8_t *) * j->n);
+  unsigned *idx = malloc(sizeof(unsigned) * j->n);
+  for (unsigned c = j->first; c < j->last; c++) {
+    const uint8_t *src = j->data + (size_t)c * j->len;
+    size_t b, pad;
+    if (zo_encode(j->k, j->n, src, j->len, shares, &b, &pad) != 0) {
+      j->bad++;
+      continue;
+    }
+    unsigned m = 0;
+    for (unsigned i = 0; i < j->n; i++) {
+      int lost = 0;
+      for (unsigned e = 0; e < j->nerased; e++) lost |= j->erased[e] == i;
+      if (!lost) {
+        sv[m] = shares + (size_t)i * B;
+        idx[m++] = i;
+      }
+    }
+    if (zo_decode(j->k, j->n, sv, idx, m, B, pad, out) != 0 || memcmp(out, src, j->len))
+      j->bad++;
+  }
+  free(shares);
+  free(out);
+  free(sv);
+  free(idx);
+  return NULL;
+}
+
+int zo_roundtrip_many(unsigned k, unsigned n, const uint8_t *data, size_t len,
+                      unsigned nchunks, const unsigned *erased, unsigned nerased,
+                      int threads) {
+  zo_init();
+  if (k < 1 || n < 1 || n > 256 || k > n || len == 0) return -1;
+  if (threads <= 0) threads = 1;
+  if ((unsigned)threads > nchunks) threads = (int)nchunks;
+  pthread_t *tid = malloc(sizeof(pthread_t) * threads);
+  rt_job *jobs = calloc(threads, sizeof(rt_job));
+  unsigned per = (nchunks + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (rt_job){k, n, t * per < nchunks ? t * per : nchunks,
+                       (t + 1) * per < nchunks ? (t + 1) * per : nchunks, nerased, erased,
+                       data, len, 0};
+    pthread_create(&tid[t], NULL, rt_worker, &jobs[t]);
+  }
+  int bad = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(tid[t], NULL);
+    bad += jobs[t].bad;
+  }
+  free(tid);
+  free(jobs);
+  return bad;
+}

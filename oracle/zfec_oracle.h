@@ -79,6 +79,15 @@ void zo_splitmix_fill(uint64_t seed, uint8_t *out, size_t len);
 int zo_encode_many(unsigned k, unsigned n, const uint8_t *data, size_t len,
                    unsigned nchunks, uint8_t *parity, int threads);
 
+/* Multi-threaded encode + decode round trips of nchunks independent chunks
+ * of len bytes (data back to back), losing the `nerased` shares listed in
+ * erased[] (first k survivors by index decode). Returns the number of
+ * chunks whose round trip failed (0 = all bit-exact), -1 on bad input.
+ * CPU baseline "nproc threads" figure. */
+int zo_roundtrip_many(unsigned k, unsigned n, const uint8_t *data, size_t len,
+                      unsigned nchunks, const unsigned *erased, unsigned nerased,
+                      int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,13 @@ def _declare(L):
     L.storb_rs_decode_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
                                             C.POINTER(C.c_uint32), C.c_uint32, vp, sz, vp,
                                             sz, vp, sz, vp]
+    L.storb_rs_repair_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
+                                            C.POINTER(C.c_uint32), C.c_uint32,
+                                            C.POINTER(C.c_uint32), C.c_uint32, vp, sz, vp,
+                                            sz, vp]
+    L.storb_rs_repair.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(vp),
+                                  C.POINTER(C.c_uint32), C.c_uint32, sz,
+                                  C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(vp)]
     L.storb_rs_apply_dev.argtypes = [vp, C.c_uint32, C.c_uint32, vp, C.POINTER(vp),
                                      C.POINTER(sz), C.POINTER(vp), C.POINTER(sz), sz,
                                      C.c_uint32, vp]
@@ -216,6 +223,21 @@ class Context:
         self._check(rc, "storb_rs_decode")
         return out[:outlen].tobytes()
 
+    def repair(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
+               targets: Sequence[int]) -> list[bytes]:
+        """Regenerate shares `targets` (data or parity) of one stripe from the
+        first k of the given shares by index (decode-based repair)."""
+        arrs = [_as_u8(s) for s in shares]
+        ptrs = (vp * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
+        ids = (C.c_uint32 * max(len(idx), 1))(*idx)
+        outs = [np.zeros(max(block, 1), dtype=np.uint8) for _ in targets]
+        optr = (vp * max(len(outs), 1))(*[o.ctypes.data for o in outs])
+        tg = (C.c_uint32 * max(len(targets), 1))(*targets)
+        rc = lib().storb_rs_repair(self._h, k, n, ptrs, ids, len(arrs), block, tg,
+                                   len(targets), optr)
+        self._check(rc, "storb_rs_repair")
+        return [o[:block].tobytes() for o in outs]
+
     def encode_chunks(self, k: int, n: int, data: np.ndarray, chunk_len: int,
                       nchunks: int) -> np.ndarray:
         buf = _as_u8(data)
@@ -258,6 +280,18 @@ class Context:
                                              len(share_idx), d_data, data_stride, d_parity,
                                              parity_stride, d_out, out_stride, self._s(stream))
         self._check(rc, "storb_rs_decode_batch_dev")
+
+    def repair_batch_dev(self, k: int, n: int, block: int, nstripes: int,
+                         share_idx: Sequence[int], targets: Sequence[int], d_data: int,
+                         d_parity: int, data_stride: int = 0, parity_stride: int = 0,
+                         stream: Optional[int] = None):
+        ids = (C.c_uint32 * max(len(share_idx), 1))(*share_idx)
+        tg = (C.c_uint32 * max(len(targets), 1))(*targets)
+        rc = lib().storb_rs_repair_batch_dev(self._h, k, n, block, nstripes, ids,
+                                             len(share_idx), tg, len(targets), d_data,
+                                             data_stride, d_parity, parity_stride,
+                                             self._s(stream))
+        self._check(rc, "storb_rs_repair_batch_dev")
 
     def apply_dev(self, coef: np.ndarray, d_in: Sequence[int], in_stride: Sequence[int],
                   d_out: Sequence[int], out_stride: Sequence[int], block: int,

@@ -49,6 +49,7 @@ struct Tune {
   static constexpr bool BAR = false;
   static constexpr int G = KM < 8 ? KM : 8;
   static constexpr bool TL = KM >= 8;
+  static constexpr bool PAIR = KM == 8 && RM <= 4;  // measured +2.5 % (W2)
 };
 
 template <int KM>
@@ -116,7 +117,7 @@ __device__ __forceinline__ void load_group(const ApplyArgs &a, uint32_t k, uint3
 // VGPRs and scratch spills at k = 8, r = 4). Per input the selectors are
 // computed once; per (row, input) the table is read from SGPRs right
 // before its v_perm_b32s, and a sched_barrier stops the hoisting.
-template <int KM, int RM, int T, int U, bool BAR, int G, bool GUARD>
+template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD>
 __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tabs,
                                           uint32_t k, uint32_t r, uint32_t cols,
                                           uint32_t stripe, uint32_t c0) {
@@ -133,35 +134,79 @@ __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tab
   for (int g = 0; g < NG; g++) {
     if (g + 1 < NG)
       load_group<KM, G, T, U, GUARD>(a, k, cols, stripe, c0, g + 1, buf[(g + 1) & 1]);
+    if constexpr (PAIR) {
+      // Inputs two at a time: per (row, dword) the six v_perm_b32 lookups
+      // of inputs j and j+1 fold into acc with three 3-input XORs (instead
+      // of four XOR instructions); tables are read per row (LDS / SGPR)
+      // just before use so their registers do not scale with RM.
 #pragma unroll
-    for (int jj = 0; jj < G; jj++) {
-      const int j = g * G + jj;
-      if (j >= static_cast<int>(k)) continue;
-      uint32_t s0[U][4], s1[U][4], s2[U][4];
+      for (int jj = 0; jj < G; jj += 2) {
+        const int j = g * G + jj;
+        if (j >= static_cast<int>(k)) continue;
+        const bool two = jj + 1 < G && j + 1 < static_cast<int>(k);
+        uint32_t s0[2][U][4], s1[2][U][4], s2[2][U][4];
 #pragma unroll
-      for (int u = 0; u < U; u++)
+        for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-          const uint32_t d = buf[g & 1][jj][u][w];
-          s0[u][w] = d & 0x07070707u;
-          s1[u][w] = (d >> 3) & 0x07070707u;
-          s2[u][w] = (d >> 6) & 0x03030303u;
+          for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+              const uint32_t d = (h == 0 || two) ? buf[g & 1][jj + h][u][w] : 0u;
+              s0[h][u][w] = d & 0x07070707u;
+              s1[h][u][w] = (d >> 3) & 0x07070707u;
+              s2[h][u][w] = (d >> 6) & 0x03030303u;
+            }
+#pragma unroll
+        for (int i = 0; i < RM; i++) {
+          const PermTab ta = tabs[j * RM + i];
+          const PermTab tb = two ? tabs[(j + 1) * RM + i] : PermTab{};
+#pragma unroll
+          for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+              uint32_t x = acc[i][u][w];
+              x = xor3(x, __builtin_amdgcn_perm(ta.t0hi, ta.t0lo, s0[0][u][w]),
+                       __builtin_amdgcn_perm(ta.t1hi, ta.t1lo, s1[0][u][w]));
+              x = xor3(x, __builtin_amdgcn_perm(0u, ta.t2, s2[0][u][w]),
+                       __builtin_amdgcn_perm(tb.t0hi, tb.t0lo, s0[1][u][w]));
+              x = xor3(x, __builtin_amdgcn_perm(tb.t1hi, tb.t1lo, s1[1][u][w]),
+                       __builtin_amdgcn_perm(0u, tb.t2, s2[1][u][w]));
+              acc[i][u][w] = x;
+            }
+          if constexpr (BAR) __builtin_amdgcn_sched_barrier(0);  // per-row tables
         }
-      // Tables are stored [input][RM rows], rows >= r zero-padded by the
-      // host: no per-row guard, so input j is one basic block in which all
-      // RM table loads issue together and overlap the v_perm work (per-row
-      // guards made every coefficient wait out a full load latency).
-      PermTab t[RM];
+      }
+    } else {
 #pragma unroll
-      for (int i = 0; i < RM; i++) t[i] = tabs[j * RM + i];
-#pragma unroll
-      for (int i = 0; i < RM; i++)
+      for (int jj = 0; jj < G; jj++) {
+        const int j = g * G + jj;
+        if (j >= static_cast<int>(k)) continue;
+        uint32_t s0[U][4], s1[U][4], s2[U][4];
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
-          for (int w = 0; w < 4; w++)
-            acc[i][u][w] = gf_madd_perm(acc[i][u][w], t[i], s0[u][w], s1[u][w], s2[u][w]);
-      if constexpr (BAR) __builtin_amdgcn_sched_barrier(0);
+          for (int w = 0; w < 4; w++) {
+            const uint32_t d = buf[g & 1][jj][u][w];
+            s0[u][w] = d & 0x07070707u;
+            s1[u][w] = (d >> 3) & 0x07070707u;
+            s2[u][w] = (d >> 6) & 0x03030303u;
+          }
+        // Tables are stored [input][RM rows], rows >= r zero-padded by the
+        // host: no per-row guard, so input j is one basic block in which all
+        // RM table loads issue together and overlap the v_perm work (per-row
+        // guards made every coefficient wait out a full load latency).
+        PermTab t[RM];
+#pragma unroll
+        for (int i = 0; i < RM; i++) t[i] = tabs[j * RM + i];
+#pragma unroll
+        for (int i = 0; i < RM; i++)
+#pragma unroll
+          for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int w = 0; w < 4; w++)
+              acc[i][u][w] = gf_madd_perm(acc[i][u][w], t[i], s0[u][w], s1[u][w], s2[u][w]);
+        if constexpr (BAR) __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
 
@@ -186,7 +231,7 @@ __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tab
 // scalar branches; they also split the body into basic blocks, which keeps
 // the scheduler from hoisting every table load and selector (a guard-free
 // "exact" specialisation measured 181-256 VGPRs and scratch spills).
-template <int KM, int RM, int T, int U, bool BAR, int G, bool TL>
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
 __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
   constexpr uint32_t TILE = T * U;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
@@ -203,20 +248,20 @@ __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
     tabs = lds_ptab;
   }
   if (base + TILE <= cols)
-    perm_tile<KM, RM, T, U, BAR, G, false>(a, tabs, a.k, a.r, cols, stripe,
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, false>(a, tabs, a.k, a.r, cols, stripe,
                                                base + threadIdx.x);
   else
-    perm_tile<KM, RM, T, U, BAR, G, true>(a, tabs, a.k, a.r, cols, stripe,
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, true>(a, tabs, a.k, a.r, cols, stripe,
                                               base + threadIdx.x);
 }
 
-template <int KM, int RM, int T, int U, bool BAR, int G, bool TL>
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
 hipError_t launch_perm(const ApplyArgs &a, hipStream_t s) {
   const uint64_t cols = a.block >> 4;
   const uint64_t blocks = ((cols + T * U - 1) / (T * U)) * a.nstripes;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL>), dim3(blocks), dim3(T), 0,
+  hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR>), dim3(blocks), dim3(T), 0,
                      s, a);
   return hipGetLastError();
 }

@@ -288,6 +288,41 @@ int decode_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   return STORB_RS_OK;
 }
 
+// Repair rows (decode-based repair): target share t is
+// enc[t] * D^-1 over the k slot shares, where D holds the slot rows of enc.
+// For a data target that is exactly decode_rows' row; for a parity target it
+// re-encodes the rebuilt data in one pass. Targets must be distinct and must
+// not be one of the k shares read (they are written in place).
+int repair_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                const std::vector<uint32_t> &slot_idx, const uint32_t *targets,
+                uint32_t ntargets, std::vector<uint8_t> &coef) {
+  std::vector<uint8_t> seen(n, 0);
+  for (uint32_t s = 0; s < k; s++) seen[slot_idx[s]] = 1;
+  for (uint32_t r = 0; r < ntargets; r++) {
+    if (targets[r] >= n) return fail(ctx, STORB_RS_EINVAL, "repair target index >= n");
+    if (seen[targets[r]] == 1)
+      return fail(ctx, STORB_RS_EINVAL, "repair target is one of the k shares read");
+    if (seen[targets[r]] == 2) return fail(ctx, STORB_RS_EINVAL, "duplicate repair target");
+    seen[targets[r]] = 2;
+  }
+  const std::vector<uint8_t> &enc = cached_enc(k, n);
+  std::vector<uint8_t> d(static_cast<size_t>(k) * k, 0);
+  for (uint32_t s = 0; s < k; s++)
+    std::memcpy(&d[static_cast<size_t>(s) * k], &enc[static_cast<size_t>(slot_idx[s]) * k], k);
+  if (!gf_invert(d, k)) return fail(ctx, STORB_RS_EINVAL, "singular decode matrix");
+  const GF256 &g = gf();
+  coef.assign(static_cast<size_t>(ntargets) * k, 0);
+  for (uint32_t r = 0; r < ntargets; r++) {
+    const uint8_t *e = &enc[static_cast<size_t>(targets[r]) * k];
+    for (uint32_t s = 0; s < k; s++) {
+      if (!e[s]) continue;
+      const uint8_t *row = &d[static_cast<size_t>(s) * k];
+      for (uint32_t c = 0; c < k; c++) coef[static_cast<size_t>(r) * k + c] ^= g.mul(e[s], row[c]);
+    }
+  }
+  return STORB_RS_OK;
+}
+
 // NULL is the HIP null stream (ordered with the device's legacy default
 // stream, which is also PyTorch's default stream), not the context's own.
 hipStream_t pick_stream(storb_rs_ctx *, void *s) {
@@ -509,6 +544,50 @@ int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t 
                ins.data(), out.data(), outs.data(), block, nstripes, s);
 }
 
+int storb_rs_repair_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                              uint32_t nstripes, const uint32_t *share_idx,
+                              uint32_t nshares, const uint32_t *targets, uint32_t ntargets,
+                              uint8_t *d_data, size_t data_stride, uint8_t *d_parity,
+                              size_t parity_stride, void *hip_stream) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (!share_idx || (ntargets && !targets)) return fail(ctx, STORB_RS_EINVAL, "null argument");
+  if (data_stride == 0) data_stride = static_cast<size_t>(k) * block;
+  if (parity_stride == 0) parity_stride = static_cast<size_t>(n - k) * block;
+  std::vector<uint32_t> slot_idx, slot_pos;
+  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint8_t> coef;
+  rc = repair_rows(ctx, k, n, slot_idx, targets, ntargets, coef);
+  if (rc) return rc;
+  if (ntargets == 0 || block == 0 || nstripes == 0) return STORB_RS_OK;
+  auto where = [&](uint32_t id, uint8_t *&p, size_t &stride) -> bool {
+    if (id < k) {
+      p = d_data ? d_data + static_cast<size_t>(id) * block : nullptr;
+      stride = data_stride;
+    } else {
+      p = d_parity ? d_parity + static_cast<size_t>(id - k) * block : nullptr;
+      stride = parity_stride;
+    }
+    return p != nullptr;
+  };
+  std::vector<const uint8_t *> in(k);
+  std::vector<size_t> ins(k), outs(ntargets);
+  std::vector<uint8_t *> out(ntargets);
+  for (uint32_t c = 0; c < k; c++) {
+    uint8_t *p;
+    if (!where(slot_idx[c], p, ins[c])) return fail(ctx, STORB_RS_EINVAL, "share in null region");
+    in[c] = p;
+  }
+  for (uint32_t r = 0; r < ntargets; r++)
+    if (!where(targets[r], out[r], outs[r]))
+      return fail(ctx, STORB_RS_EINVAL, "target in null region");
+  DeviceGuard g(ctx->device);
+  return apply(ctx, k, ntargets, coef.data(), in.data(), ins.data(), out.data(), outs.data(),
+               block, nstripes, pick_stream(ctx, hip_stream));
+}
+
 // Host BLAKE3: chunks in order with a stack of complete subtrees; the last
 // chunk is folded right to left so the final parent carries ROOT.
 void storb_blake3(const uint8_t *data, size_t len, uint8_t out[32]) {
@@ -669,6 +748,50 @@ int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
                               hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   for (uint32_t r = 0; r < e; r++) put(missing[r], ctx->pin_out.p + static_cast<size_t>(r) * S);
+  return STORB_RS_OK;
+}
+
+int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+                    const uint32_t *share_idx, uint32_t nshares, size_t block,
+                    const uint32_t *targets, uint32_t ntargets, uint8_t *const *out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (!shares || !share_idx || (ntargets && (!targets || !out)) || block == 0)
+    return fail(ctx, STORB_RS_EINVAL, "repair: bad arguments");
+  std::vector<uint32_t> slot_idx, slot_pos;
+  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint8_t> coef;
+  rc = repair_rows(ctx, k, n, slot_idx, targets, ntargets, coef);
+  if (rc || ntargets == 0) return rc;
+  const size_t S = round_up(block, kAlign);
+  DeviceGuard g(ctx->device);
+  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(ntargets) * S));
+  HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + ntargets) * S));
+  for (uint32_t c = 0; c < k; c++) {
+    std::memcpy(ctx->pin_in.p + static_cast<size_t>(c) * S, shares[slot_pos[c]], block);
+    std::memset(ctx->pin_in.p + static_cast<size_t>(c) * S + block, 0, S - block);
+  }
+  hipStream_t s = ctx->stream;
+  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
+  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                              hipMemcpyHostToDevice, s));
+  std::vector<const uint8_t *> in(k);
+  std::vector<uint8_t *> o(ntargets);
+  std::vector<size_t> ins(k, static_cast<size_t>(k) * S),
+      outs(ntargets, static_cast<size_t>(ntargets) * S);
+  for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
+  for (uint32_t r = 0; r < ntargets; r++) o[r] = dout + static_cast<size_t>(r) * S;
+  rc = apply(ctx, k, ntargets, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1,
+             s);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(ntargets) * S,
+                              hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  for (uint32_t r = 0; r < ntargets; r++)
+    std::memcpy(out[r], ctx->pin_out.p + static_cast<size_t>(r) * S, block);
   return STORB_RS_OK;
 }
 

@@ -214,6 +214,63 @@ def test_apply_dev_regenerates_a_lost_share(ctx):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("k,n,lost", [(4, 6, (0, 5)), (4, 6, (4, 5)), (8, 12, (0, 3, 10)),
+                                      (8, 12, (9, 10, 11)), (16, 24, (0, 7, 15, 16, 20, 23)),
+                                      (2, 3, (2,)), (1, 2, (0,)), (40, 60, (1, 2, 45, 59)),
+                                      (17, 40, tuple(range(17, 40)))])
+def test_dev_repair_batch_regenerates_lost_shares(ctx, k, n, lost):
+    """storb_rs_repair_batch_dev: lost data AND parity shares rebuilt in
+    place from the first k survivors; each must equal the oracle's share."""
+    B, ns = 1040, 5
+    host = rnd(ns * k * B, 31 * k + n)
+    data = to_dev(host)
+    par = torch.zeros(ns * (n - k) * B, dtype=torch.uint8, device=DEV)
+    ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
+    ctx.sync()
+    want_par = par.cpu().numpy().copy()
+    for s in range(ns):  # the encode itself against the oracle
+        w, _, _ = oracle_parity(k, n, host[s * k * B:(s + 1) * k * B])
+        assert np.array_equal(want_par.reshape(ns, n - k, B)[s], w)
+    dv, pv = data.view(ns, k, B), par.view(ns, n - k, B)
+    for t in lost:
+        (dv[:, t] if t < k else pv[:, t - k]).fill_(0xA5)
+    survivors = [i for i in range(n) if i not in lost]
+    random.Random(n).shuffle(survivors)
+    targets = list(lost)
+    random.Random(k).shuffle(targets)
+    ctx.repair_batch_dev(k, n, B, ns, survivors, targets, data.data_ptr(), par.data_ptr())
+    ctx.sync()
+    assert np.array_equal(data.cpu().numpy(), host)
+    assert np.array_equal(par.cpu().numpy(), want_par)
+
+
+def test_repair_rejects_bad_targets(ctx):
+    d = torch.zeros(4 * 64, dtype=torch.uint8, device=DEV)
+    p = torch.zeros(2 * 64, dtype=torch.uint8, device=DEV)
+    for targets in ([1], [6], [5, 5]):  # a share read / out of range / repeated
+        with pytest.raises(_lib.StorbRsError) as e:
+            ctx.repair_batch_dev(4, 6, 64, 1, [0, 1, 2, 3], targets, d.data_ptr(), p.data_ptr())
+        assert e.value.code == _lib.EINVAL
+    with pytest.raises(_lib.StorbRsError) as e:
+        ctx.repair_batch_dev(4, 6, 64, 1, [0, 1, 2], [4], d.data_ptr(), p.data_ptr())
+    assert e.value.code == _lib.ENOTENOUGH
+
+
+@pytest.mark.parametrize("k,n", [(4, 6), (8, 12), (16, 24), (3, 5)])
+def test_host_repair_matches_oracle(ctx, k, n):
+    rng = random.Random(k * n)
+    data = rnd(k * 777 + 5, k + 3 * n)
+    shares, B, _ = coracle.encode(k, n, data)
+    for _ in range(8):
+        have = rng.sample(range(n), k + rng.randrange(0, n - k + 1))
+        used = sorted(have)[:k]
+        targets = rng.sample([i for i in range(n) if i not in used],
+                             rng.randrange(1, n - k + 1))
+        got = ctx.repair(k, n, [shares[i] for i in have], have, B, targets)
+        for t, g in zip(targets, got):
+            assert g == shares[t].tobytes(), (k, n, have, t)
+
+
 def test_fill_splitmix_matches_oracle(ctx):
     for L, cnt, stride in [(1 << 20, 3, 1 << 20), (13, 5, 16), (1001, 2, 1001)]:
         buf = torch.zeros(cnt * stride, dtype=torch.uint8, device=DEV)

@@ -264,3 +264,12 @@ def test_reference_single_chunk_zeros():
     assert (c["k"], c["m"]) == (1, 2)
     keep = c["pieces"][1:]  # only the parity piece survives
     assert co.decode(1, 2, [p[2] for p in keep], [1], c["B"], c["padlen"]) == d.tobytes()
+
+
+def test_threaded_roundtrip_baseline_path():
+    # bench.py's threaded CPU baseline leg: every chunk must round-trip.
+    data = np.concatenate([co.splitmix_bytes(i, 12345) for i in range(12)])
+    assert co.roundtrip_many(4, 6, data, 12345, 12, [0, 1], 4) == 0
+    assert co.roundtrip_many(16, 24, data, 12345, 12, [0, 3, 5, 7, 9, 11, 13, 15], 3) == 0
+    # losing more than n-k shares is a failure for every chunk
+    assert co.roundtrip_many(4, 6, data, 12345, 12, [0, 1, 2], 2) == 12

@@ -58,20 +58,20 @@ struct W {
   bool inplace = false;  // decode layout of bench --config 3 (see below)
 };
 
-template <int KM, int RM, int T, int U, bool BAR, int G, bool TL = false>
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL = false, bool PAIR = false>
 V mk() {
-  char buf[96];
-  std::snprintf(buf, sizeof buf, "<%d,%d> T=%d U=%d BAR=%d G=%d TL=%d", KM, RM, T, U, (int)BAR,
-                G, (int)TL);
+  char buf[112];
+  std::snprintf(buf, sizeof buf, "<%d,%d> T=%d U=%d BAR=%d G=%d TL=%d PAIR=%d", KM, RM, T, U,
+                (int)BAR, G, (int)TL, (int)PAIR);
   return V{buf, [](const ApplyArgs &a, hipStream_t s) {
-             return launch_perm<KM, RM, T, U, BAR, G, TL>(a, s);
+             return launch_perm<KM, RM, T, U, BAR, G, TL, PAIR>(a, s);
            }, {}};
 }
 
 template <int KM, int RM>
 V product() {
   using C = Tune<KM, RM>;
-  V v = mk<KM, RM, C::T, C::U, C::BAR, C::G, C::TL>();
+  V v = mk<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>();
   v.name = "product " + v.name;
   return v;
 }
@@ -80,19 +80,16 @@ template <int KM, int RM>
 void add_all(std::vector<V> &v) {
   constexpr int GM = KM < 8 ? KM : 8;
   v.push_back(product<KM, RM>());
-  v.push_back(mk<KM, RM, 256, 1, false, GM, false>());
-  v.push_back(mk<KM, RM, 256, 1, true, GM, false>());
-  v.push_back(mk<KM, RM, 256, 1, false, GM, true>());
-  v.push_back(mk<KM, RM, 256, 1, true, GM, true>());
-  v.push_back(mk<KM, RM, 128, 1, true, GM, false>());
-  v.push_back(mk<KM, RM, 128, 1, true, GM, true>());
-  v.push_back(mk<KM, RM, 256, 2, true, GM, false>());
-  v.push_back(mk<KM, RM, 256, 2, true, GM, true>());
+  v.push_back(mk<KM, RM, 256, 1, false, GM, KM >= 8, false>());
+  v.push_back(mk<KM, RM, 256, 1, false, GM, KM >= 8, true>());
+  v.push_back(mk<KM, RM, 256, 1, true, GM, KM >= 8, true>());
+  v.push_back(mk<KM, RM, 256, 1, false, GM, !(KM >= 8), true>());
+  v.push_back(mk<KM, RM, 128, 1, false, GM, KM >= 8, true>());
+  v.push_back(mk<KM, RM, 256, 2, false, GM, KM >= 8, true>());
   if constexpr (KM >= 8) {
-    v.push_back(mk<KM, RM, 256, 1, true, 4, false>());
-    v.push_back(mk<KM, RM, 256, 1, true, 4, true>());
-    v.push_back(mk<KM, RM, 64, 1, true, 4, true>());
-    v.push_back(mk<KM, RM, 128, 1, true, 4, true>());
+    v.push_back(mk<KM, RM, 256, 1, false, 4, true, true>());
+    v.push_back(mk<KM, RM, 256, 1, false, 4, true, false>());
+    v.push_back(mk<KM, RM, 128, 1, false, 8, true, false>());
   }
 }
 
