@@ -51,12 +51,16 @@ SEED_BASE = 0x5709B
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, choices=[2, 3, 4], default=2)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
+                   help="BASELINE config; 5 = the device-resident GPU half of config 5 "
+                        "(1 GiB object -> 128 x 8 MiB chunks, storb k=16, m=24)")
     p.add_argument("--chunks", type=int, default=None, help="chunks per GPU (config 2/3)")
     p.add_argument("--objects", type=int, default=10000, help="total objects (config 4)")
-    p.add_argument("--kernel", choices=["perm", "lds"], default="perm")
+    p.add_argument("--kernel", choices=["auto", "perm", "lds"], default="auto",
+                   help="auto = what the product runs (bit-sliced encoder for k=16/32, "
+                        "v_perm tables otherwise); perm / lds force a table kernel")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--no-check", action="store_true")
@@ -140,21 +144,38 @@ def cpu_model():
     return "unknown"
 
 
-def copy_ceiling(dev, stream, nbytes=1 << 30, reps=5):
-    """Measured device-to-device copy rate (read + write bytes / time), the
-    practical HBM ceiling SURVEY 8(d) asks to report beside the 8 TB/s spec."""
+def copy_ceiling(ctx, dev, stream, nbytes=1 << 30, reps=5):
+    """Measured device-to-device copy rates (read + write bytes / time), the
+    practical HBM ceiling SURVEY 8(d) asks to report beside the 8 TB/s spec:
+    our own kernel as a copy (RS apply with k=1 and coefficient 1: the same
+    load/store path, no GF work) and torch's copy_ for comparison."""
     src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
+    blk = 1 << 20
+    one = np.ones((1, 1), dtype=np.uint8)
+
+    def ours():
+        ctx.apply_dev(one, [src.data_ptr()], [blk], [dst.data_ptr()], [blk], blk,
+                      nbytes // blk, stream=stream.cuda_stream)
+
+    def theirs():
+        dst.copy_(src)
+
+    rates = {}
     with torch.cuda.stream(stream):
         src.random_(0, 256)
-        dst.copy_(src)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            dst.copy_(src)
-        e1.record(stream)
-    stream.synchronize()
-    return round(2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+        for name, f in (("rs_apply_copy", ours), ("torch_copy", theirs)):
+            f()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                f()
+            e1.record(stream)
+            stream.synchronize()
+            rates[name] = round(2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    if not torch.equal(src, dst):
+        raise SystemExit("copy ceiling: copy mismatch")
+    return rates
 
 
 def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256):
@@ -198,6 +219,20 @@ def shard_hash_rate(ctx, w, stream, reps=3):
             "what": "blake3 (Storb piece id) of all data+parity shards, batched kernel"}
 
 
+def kernel_names(kernel, w):
+    """The kernels the legs launch (rs_bitslice.hpp / rs_device.hpp)."""
+    names = {}
+    table = "lds" if kernel == "lds" else "perm"
+    if "encode" in w.legs:
+        bits = kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48))
+        names["encode"] = (f"rs_encode_bitslice<{w.k},{w.n}>" if bits
+                           else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")
+    if "decode" in w.legs:
+        e = sum(1 for x in w.erased if x < w.k)
+        names["decode"] = f"rs_apply_{table}<{min(w.k, 32)},{e}>"
+    return names
+
+
 class Workload:
     """Device-resident buffers + the launches of one step."""
 
@@ -223,6 +258,16 @@ class Workload:
             self.scaling = "weak"
             self.workload = (f"RS(k=8,m=4) [storb k=8,m=12] decode, erased [0, 3, 5], "
                              f"survivors first 8 by index, {N} x 256 KiB chunks per GPU")
+        elif c == 5:
+            self.k, self.n, chunk, self.erased = 16, 24, 8 << 20, [0, 1]
+            N = a.chunks or 128
+            seed0 = SEED_BASE + rank * N
+            self.legs = ("encode", "decode")
+            self.metric = ("GiB/s device-resident RS encode+decode, 8 MiB chunks k=16 m=8 "
+                           "(Storb's geometry for a 1 GiB object)")
+            self.scaling = "weak"
+            self.workload = (f"RS(k=16,m=8) [storb k=16,m=24] encode + decode(erased [0, 1]) "
+                             f"of {N} x 8 MiB chunks (a 1 GiB object) per GPU, device-resident")
         else:
             self.k, self.n, chunk, self.erased = 4, 6, 1 << 20, []
             mine = partition.objects_for_rank(a.objects, rank, world)
@@ -291,7 +336,8 @@ def main():
             dist.init_process_group(a.dist_backend)
 
     ctx = _lib.Context(local)
-    ctx.set_kernel(_lib.KERNEL_LDS if a.kernel == "lds" else _lib.KERNEL_PERM)
+    ctx.set_kernel({"auto": _lib.KERNEL_AUTO, "perm": _lib.KERNEL_PERM,
+                    "lds": _lib.KERNEL_LDS}[a.kernel])
     stream = torch.cuda.Stream(device=dev)
     sp = stream.cuda_stream
     w = Workload(a, ctx, dev, sp, rank, world)
@@ -357,7 +403,8 @@ def main():
     if a.config == 2 and os.path.exists(tpath):
         try:
             t = json.load(open(tpath))
-            if (t.get("kernel") == a.kernel and t.get("chunks") == w.N
+            if (t.get("kernel") in (a.kernel, "perm" if a.kernel == "auto" else None)
+                    and t.get("chunks") == w.N
                     and t.get("chunk_bytes") == w.chunk):
                 traffic = t.get("bytes_per_launch")
         except Exception:
@@ -391,8 +438,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": f"rs_apply_{a.kernel}<{min(w.k, 32)},"
-                      f"{(w.n - w.k) if 'encode' in w.legs else len(w.erased)}> (all launches)",
+            "kernel": kernel_names(a.kernel, w),
             "leg_ms": {leg: round(ms, 4) for leg, ms in zip(w.legs, leg_ms)},
             "alg_bytes_per_launch": alg,
             "copy_ceiling_gbs": None,
@@ -400,7 +446,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
-        out["roofline"]["copy_ceiling_gbs"] = copy_ceiling(dev, stream)
+        out["roofline"]["copy_ceiling_gbs"] = copy_ceiling(ctx, dev, stream)
         if a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.erased), a.cpu_seconds,
                                                do_encode="encode" in w.legs,
@@ -409,9 +455,10 @@ def main():
             if a.config == 2:
                 out["cpu_baseline_threads"] = cpu_baseline_threads(w.k, w.n, w.chunk,
                                                                    set(w.erased))
-        if not a.no_host_path and a.config == 2:
-            out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk)
-        if a.config == 2:
+        if not a.no_host_path and a.config in (2, 5):
+            out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
+                                                   nchunks=max(8, (256 << 20) // w.chunk))
+        if a.config in (2, 5):
             out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -184,8 +184,11 @@ int storb_rs_fill_splitmix_dev(storb_rs_ctx *ctx, uint8_t *d, size_t obj_len,
                                uint32_t nobj, size_t obj_stride,
                                uint64_t seed_base, void *hip_stream);
 
-/* Which kernel variant the dev calls launch (0 = auto). Benchmarks use it
- * to time the LDS-table variant beside the register-table one. */
+/* Which kernel variant the calls launch. AUTO (default): encodes of
+ * (k, n) = (16, 24) and (32, 48) -- Storb's geometry for 8-32 MiB chunks --
+ * run the bit-sliced encoder with the generator compiled in, everything else
+ * the register-table kernel. PERM / LDS force that table kernel for every
+ * call (benchmarks and the identical-output tests use them). */
 #define STORB_RS_KERNEL_AUTO 0
 #define STORB_RS_KERNEL_PERM 1 /* nibble tables in registers, v_perm_b32 */
 #define STORB_RS_KERNEL_LDS 2  /* 256-B product tables staged in LDS */

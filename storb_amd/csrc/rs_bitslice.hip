@@ -1,0 +1,18 @@
+// rs_bitslice.hip -- instantiations of the bit-sliced encoders
+// (rs_bitslice.hpp) for Storb's wide full-chunk geometries.
+#include "rs_bitslice.hpp"
+
+namespace storb_rs {
+
+bool bitslice_supported(uint32_t k, uint32_t n) {
+  return (k == 16 && n == 24) || (k == 32 && n == 48);
+}
+
+hipError_t launch_encode_bitslice(const ApplyArgs &a, uint32_t n, hipStream_t s) {
+  if (a.r != n - a.k || !vector_ok(a)) return hipErrorInvalidValue;
+  if (a.k == 16 && n == 24) return bs::launch_bitslice<16, 24>(a, s);
+  if (a.k == 32 && n == 48) return bs::launch_bitslice<32, 48>(a, s);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace storb_rs

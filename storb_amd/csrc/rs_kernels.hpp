@@ -49,6 +49,12 @@ bool vector_ok(const ApplyArgs &a);
 
 hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s);
 
+// Bit-sliced encoders with the generator compiled in (rs_bitslice.hpp) for
+// the (k, n) Storb's large objects use. a.in / a.out hold the k data and
+// n - k parity slots; needs vector_ok(a).
+bool bitslice_supported(uint32_t k, uint32_t n);
+hipError_t launch_encode_bitslice(const ApplyArgs &a, uint32_t n, hipStream_t s);
+
 hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
                                uint64_t stride, uint8_t *out, hipStream_t s);
 

@@ -228,6 +228,39 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
   return STORB_RS_OK;
 }
 
+// Parity of (k, n) = enc[k..n) * data. Under the AUTO variant the geometries
+// with a compiled-in bit-sliced encoder take it (rs_bitslice.hpp: 1.5-2.9x
+// the v_perm kernel at k = 16 / 32, where that one is VALU-bound); the rest,
+// and explicit PERM / LDS requests, go through the table kernels.
+int encode_apply(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *d_in,
+                 const size_t *in_stride, uint8_t *const *d_out, const size_t *out_stride,
+                 size_t block, uint32_t nstripes, hipStream_t s) {
+  const uint32_t p = n - k;
+  if (p == 0 || block == 0 || nstripes == 0) return STORB_RS_OK;
+  if (ctx->variant == STORB_RS_KERNEL_AUTO && bitslice_supported(k, n)) {
+    ApplyArgs a{};
+    a.k = k;
+    a.r = p;
+    for (uint32_t j = 0; j < k; j++) {
+      a.in[j] = d_in[j];
+      a.in_stride[j] = in_stride[j];
+    }
+    for (uint32_t i = 0; i < p; i++) {
+      a.out[i] = d_out[i];
+      a.out_stride[i] = out_stride[i];
+    }
+    a.block = block;
+    a.nstripes = nstripes;
+    if (vector_ok(a)) {
+      HIP_TRY(ctx, launch_encode_bitslice(a, n, s));
+      return STORB_RS_OK;
+    }
+  }
+  const std::vector<uint8_t> &enc = cached_enc(k, n);
+  return apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, d_in, in_stride, d_out,
+               out_stride, block, nstripes, s);
+}
+
 // decode_chunk selection (piece.rs:368-381): sort by index, keep first k,
 // then zfec's slot arrangement: primary share s in slot s, parity shares
 // fill the holes in index order. Returns the k slot share-indices and the
@@ -480,15 +513,14 @@ int storb_rs_encode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t 
   if (data_stride == 0) data_stride = static_cast<size_t>(k) * block;
   if (parity_stride == 0) parity_stride = static_cast<size_t>(n - k) * block;
   DeviceGuard g(ctx->device);
-  const std::vector<uint8_t> &enc = cached_enc(k, n);
   const uint32_t p = n - k;
   std::vector<const uint8_t *> in(k);
   std::vector<size_t> ins(k, data_stride), outs(p, parity_stride);
   std::vector<uint8_t *> out(p);
   for (uint32_t j = 0; j < k; j++) in[j] = d_data + static_cast<size_t>(j) * block;
   for (uint32_t i = 0; i < p; i++) out[i] = d_parity + static_cast<size_t>(i) * block;
-  return apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(), ins.data(),
-               out.data(), outs.data(), block, nstripes, pick_stream(ctx, hip_stream));
+  return encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), block,
+                      nstripes, pick_stream(ctx, hip_stream));
 }
 
 int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
@@ -683,14 +715,12 @@ int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *da
   hipStream_t s = ctx->stream;
   uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
   HIP_TRY(ctx, hipMemcpyAsync(dd, hin, static_cast<size_t>(k) * S, hipMemcpyHostToDevice, s));
-  const std::vector<uint8_t> &enc = cached_enc(k, n);
   std::vector<const uint8_t *> in(k);
   std::vector<uint8_t *> out(p);
   std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(p, static_cast<size_t>(p) * S);
   for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
   for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
-  int rc = apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(), ins.data(),
-                 out.data(), outs.data(), S, 1, s);
+  int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S, 1, s);
   if (rc) return rc;
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dp, static_cast<size_t>(p) * S,
                               hipMemcpyDeviceToHost, s));
@@ -826,7 +856,6 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch + hash_bytes));
     HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
   }
-  const std::vector<uint8_t> &enc = cached_enc(k, n);
   const uint32_t nb = (nchunks + batch - 1) / batch;
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;
@@ -887,8 +916,8 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
       std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
       for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
       for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
-      const int rc = apply(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, in.data(),
-                           ins.data(), out.data(), outs.data(), S, cn, s);
+      const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S,
+                                  cn, s);
       if (rc) return rc;
     }
     size_t back = static_cast<size_t>(p) * S * cn;

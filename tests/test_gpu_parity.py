@@ -162,6 +162,35 @@ def test_dev_encode_tiled_large_matrices(ctx, k, n, B, ns):
     dev_encode_check(ctx, k, n, B, ns)
 
 
+# Storb's wide full-chunk geometries take the bit-sliced encoder under AUTO
+# (rs_bitslice.hpp): one 16-B column, ragged tiles, exact 8 KiB tiles.
+@pytest.mark.parametrize("k,n", [(16, 24), (32, 48)])
+@pytest.mark.parametrize("B,ns", [(16, 3), (1040, 4), (8192, 3), (3 * 8192 + 48, 2),
+                                  (16 * 1024 + 1024, 2)])
+def test_dev_encode_bitslice_matches_oracle(ctx, k, n, B, ns):
+    dev_encode_check(ctx, k, n, B, ns, kernel=_lib.KERNEL_AUTO)
+
+
+@pytest.mark.parametrize("k,n,B,ns", [(16, 24, 512 << 10, 9), (32, 48, 1 << 20, 3)])
+def test_bitslice_identical_to_table_kernel(ctx, k, n, B, ns):
+    """AUTO (bit-sliced) and forced PERM (v_perm tables) encodes agree byte
+    for byte on the config-5 share size, splitmix input."""
+    data = torch.empty(ns * k * B, dtype=torch.uint8, device=DEV)
+    ctx.fill_splitmix_dev(data.data_ptr(), k * B, ns, k * B, 0x5709B)
+    outs = []
+    for kern in (_lib.KERNEL_AUTO, _lib.KERNEL_PERM):
+        ctx.set_kernel(kern)
+        par = torch.full((ns * (n - k) * B,), 0xA5, dtype=torch.uint8, device=DEV)
+        ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
+        ctx.sync()
+        outs.append(par)
+    ctx.set_kernel(_lib.KERNEL_AUTO)
+    assert torch.equal(outs[0], outs[1])
+    # and one stripe against the oracle
+    want, _, _ = oracle_parity(k, n, data[:k * B].cpu().numpy())
+    assert np.array_equal(outs[0][:(n - k) * B].cpu().numpy().reshape(n - k, B), want)
+
+
 @pytest.mark.parametrize("k,n,erased", [(8, 12, (0, 3, 5)), (8, 12, (9, 10, 11)),
                                         (4, 6, (0, 1)), (4, 6, (2, 5)), (16, 24, tuple(range(8))),
                                         (6, 9, (1, 4, 8)), (40, 60, tuple(range(0, 40, 2))),
