@@ -14,6 +14,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -23,6 +24,7 @@
 
 #include "blake3.hpp"
 #include "gf256.hpp"
+#include "host_pool.hpp"
 #include "rs_kernels.hpp"
 
 using namespace storb_rs;
@@ -117,6 +119,7 @@ struct storb_rs_ctx {
   PinBuf pin_in, pin_out;
   PinBuf pipe_in[2], pipe_out[2];
   std::map<std::vector<uint8_t>, std::unique_ptr<Tables>> tables;
+  std::unique_ptr<HostPool> pool;  // host copy workers, created on first use
 };
 
 namespace {
@@ -354,6 +357,19 @@ int repair_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     }
   }
   return STORB_RS_OK;
+}
+
+// Host copy threads: STORB_RS_HOST_THREADS, default 8 (capped by the
+// machine). The pageable <-> pinned copies of the pipelined path use them.
+HostPool &host_pool(storb_rs_ctx *ctx) {
+  if (!ctx->pool) {
+    int n = 8;
+    if (const char *e = std::getenv("STORB_RS_HOST_THREADS")) n = std::atoi(e);
+    const int hw = static_cast<int>(std::thread::hardware_concurrency());
+    if (hw > 0) n = std::min(n, hw);
+    ctx->pool = std::make_unique<HostPool>(std::max(1, std::min(n, 64)));
+  }
+  return *ctx->pool;
 }
 
 // NULL is the HIP null stream (ordered with the device's legacy default
@@ -857,18 +873,20 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
   }
   const uint32_t nb = (nchunks + batch - 1) / batch;
+  HostPool &pool = host_pool(ctx);
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;
     const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
     if (p > 0) {
       if (S == B) {
-        std::memcpy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
-                    static_cast<size_t>(cn) * p * B);
+        pool.copy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
+                  static_cast<size_t>(cn) * p * B);
       } else {
-        for (uint32_t c = 0; c < cn; c++)
+        pool.run(static_cast<int>(cn), [&](int c) {
           for (uint32_t i = 0; i < p; i++)
             std::memcpy(parity_out + ((static_cast<size_t>(c0) + c) * p + i) * B,
                         ctx->pipe_out[b].p + (static_cast<size_t>(c) * p + i) * S, B);
+        });
       }
     }
     if (hashes_out) {
@@ -893,9 +911,9 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
     uint8_t *hin = ctx->pipe_in[b].p;
     if (packed) {
-      std::memcpy(hin, data + static_cast<size_t>(c0) * chunk_len, per * cn);
+      pool.copy(hin, data + static_cast<size_t>(c0) * chunk_len, per * cn);
     } else {
-      for (uint32_t c = 0; c < cn; c++) {
+      pool.run(static_cast<int>(cn), [&](int c) {
         const uint8_t *src = data + (static_cast<size_t>(c0) + c) * chunk_len;
         for (uint32_t j = 0; j < k; j++) {
           const size_t off = static_cast<size_t>(j) * B;
@@ -904,7 +922,7 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
           if (cnt) std::memcpy(dst, src + off, cnt);
           std::memset(dst + cnt, 0, S - cnt);
         }
-      }
+      });
     }
     uint8_t *dd = ctx->pipe_dev[b].p;
     uint8_t *dp = dd + per * batch;

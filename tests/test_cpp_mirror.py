@@ -33,3 +33,13 @@ def test_cpp_mirror_reference_tests_pass():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all checks passed" in r.stdout
+
+
+def test_host_pool_copies_and_runs_every_part():
+    src = os.path.join(ROOT, "tests", "cpp", "test_host_pool.cpp")
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "test_host_pool")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-o", exe, src], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "host pool ok" in r.stdout
