@@ -116,6 +116,20 @@ int storb_rs_encode_chunks_hashed(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                                   uint32_t nchunks, uint8_t *parity_out,
                                   uint8_t *hashes_out);
 
+/* ---- page-locked host memory ------------------------------------------ */
+/* Storb fills a chunk buffer from the upload body (upload.rs:333-383) and
+ * hands it to encode_chunk (upload.rs:420). When that buffer -- and the
+ * buffer parity lands in -- is page-locked, storb_rs_encode_chunks DMAs it
+ * directly (no staging copy through the context's own pinned buffers).
+ * Memory from storb_rs_host_alloc, or a caller range made page-locked with
+ * storb_rs_host_register, qualifies; the check is by address range. */
+int storb_rs_host_alloc(size_t len, void **out);
+int storb_rs_host_free(void *p); /* only pointers from storb_rs_host_alloc */
+int storb_rs_host_register(void *p, size_t len);
+int storb_rs_host_unregister(void *p);
+/* 1 if [p, p+len) lies inside one range above, else 0. */
+int storb_rs_host_is_pinned(const void *p, size_t len);
+
 /* ---- device-resident batched variants -------------------------------- */
 /* Stripe s, data share j lives at d_data + s*data_stride + j*block; parity
  * share p at d_parity + s*parity_stride + p*block. Strides of 0 mean the

@@ -87,6 +87,11 @@ def _declare(L):
     L.storb_blake3.argtypes = [vp, sz, vp]
     L.storb_blake3.restype = None
     L.storb_rs_blake3_batch_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, vp, vp]
+    L.storb_rs_host_alloc.argtypes = [sz, C.POINTER(vp)]
+    L.storb_rs_host_free.argtypes = [vp]
+    L.storb_rs_host_register.argtypes = [vp, sz]
+    L.storb_rs_host_unregister.argtypes = [vp]
+    L.storb_rs_host_is_pinned.argtypes = [vp, sz]
     L.storb_rs_set_kernel.argtypes = [vp, C.c_int]
     L.storb_rs_sync.argtypes = [vp]
 
@@ -156,6 +161,36 @@ def _as_u8(data) -> np.ndarray:
     if isinstance(data, np.ndarray):
         return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
     return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+class PinnedBuffer:
+    """Page-locked host bytes from storb_rs_host_alloc, viewed as a numpy
+    array. storb_rs_encode_chunks DMAs such buffers in place."""
+
+    def __init__(self, nbytes: int):
+        p = vp()
+        rc = lib().storb_rs_host_alloc(nbytes, C.byref(p))
+        if rc != OK:
+            raise StorbRsError(rc, "storb_rs_host_alloc")
+        self._p = p
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(nbytes,))
+
+    def free(self):
+        if getattr(self, "_p", None):
+            self.array = None
+            lib().storb_rs_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def host_is_pinned(arr: np.ndarray) -> bool:
+    return bool(lib().storb_rs_host_is_pinned(arr.ctypes.data, arr.nbytes))
 
 
 class Context:
@@ -239,11 +274,14 @@ class Context:
         return [o[:block].tobytes() for o in outs]
 
     def encode_chunks(self, k: int, n: int, data: np.ndarray, chunk_len: int,
-                      nchunks: int) -> np.ndarray:
+                      nchunks: int, out: Optional[np.ndarray] = None) -> np.ndarray:
         buf = _as_u8(data)
         assert buf.size >= chunk_len * nchunks
         B = block_size(k, chunk_len)
-        out = np.empty(nchunks * (n - k) * B, dtype=np.uint8)
+        if out is None:
+            out = np.empty(nchunks * (n - k) * B, dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.flags.c_contiguous
+        assert out.size >= nchunks * (n - k) * B
         rc = lib().storb_rs_encode_chunks(self._h, k, n, buf.ctypes.data, chunk_len,
                                           nchunks, out.ctypes.data)
         self._check(rc, "storb_rs_encode_chunks")

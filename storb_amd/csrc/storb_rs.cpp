@@ -105,6 +105,22 @@ const std::vector<uint8_t> &cached_enc(uint32_t k, uint32_t n) {
 
 std::atomic<int> g_rr{0};
 
+// Page-locked host ranges the caller obtained through storb_rs_host_alloc or
+// storb_rs_host_register. The pipelined host path DMAs straight from / into
+// such ranges instead of staging through its own pinned buffers.
+std::mutex g_pin_mu;
+std::map<uintptr_t, std::pair<size_t, bool>> g_pinned;  // base -> (len, allocated here)
+
+bool range_pinned(const void *p, size_t len) {
+  if (!p || len == 0) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pinned.upper_bound(a);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return a - it->first + len <= it->second.first;
+}
+
 }  // namespace
 
 struct storb_rs_ctx {
@@ -493,6 +509,51 @@ int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant) {
   return STORB_RS_OK;
 }
 
+int storb_rs_host_alloc(size_t len, void **out) {
+  if (!out || len == 0) return STORB_RS_EINVAL;
+  *out = nullptr;
+  void *p = nullptr;
+  const hipError_t e = hipHostMalloc(&p, len, hipHostMallocPortable);
+  if (e != hipSuccess) return e == hipErrorOutOfMemory ? STORB_RS_ENOMEM : STORB_RS_EDEVICE;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[reinterpret_cast<uintptr_t>(p)] = {len, true};
+  *out = p;
+  return STORB_RS_OK;
+}
+
+int storb_rs_host_free(void *p) {
+  if (!p) return STORB_RS_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pinned.find(reinterpret_cast<uintptr_t>(p));
+    if (it == g_pinned.end() || !it->second.second) return STORB_RS_EINVAL;
+    g_pinned.erase(it);
+  }
+  return hipHostFree(p) == hipSuccess ? STORB_RS_OK : STORB_RS_EDEVICE;
+}
+
+int storb_rs_host_register(void *p, size_t len) {
+  if (!p || len == 0) return STORB_RS_EINVAL;
+  const hipError_t e = hipHostRegister(p, len, hipHostRegisterPortable);
+  if (e != hipSuccess) return e == hipErrorOutOfMemory ? STORB_RS_ENOMEM : STORB_RS_EDEVICE;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[reinterpret_cast<uintptr_t>(p)] = {len, false};
+  return STORB_RS_OK;
+}
+
+int storb_rs_host_unregister(void *p) {
+  if (!p) return STORB_RS_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pinned.find(reinterpret_cast<uintptr_t>(p));
+    if (it == g_pinned.end() || it->second.second) return STORB_RS_EINVAL;
+    g_pinned.erase(it);
+  }
+  return hipHostUnregister(p) == hipSuccess ? STORB_RS_OK : STORB_RS_EDEVICE;
+}
+
+int storb_rs_host_is_pinned(const void *p, size_t len) { return range_pinned(p, len) ? 1 : 0; }
+
 int storb_rs_sync(storb_rs_ctx *ctx) {
   if (!ctx) return STORB_RS_EINVAL;
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -866,9 +927,14 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
   batch = std::min(batch, nchunks);
   const size_t hash_bytes = hashes_out ? static_cast<size_t>(batch) * n * 32 : 0;
+  // Caller buffers that are page-locked (storb_rs_host_alloc / _register)
+  // are DMA'd directly: no pack copy in, no unpack copy out.
+  const bool in_direct = packed && range_pinned(data, static_cast<size_t>(nchunks) * chunk_len);
+  const bool out_direct =
+      p > 0 && S == B && range_pinned(parity_out, static_cast<size_t>(nchunks) * p * B);
   DeviceGuard g(ctx->device);
   for (int b = 0; b < 2; b++) {
-    HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
+    if (!in_direct) HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
     HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch + hash_bytes));
     HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
   }
@@ -877,7 +943,7 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;
     const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
-    if (p > 0) {
+    if (p > 0 && !out_direct) {
       if (S == B) {
         pool.copy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
                   static_cast<size_t>(cn) * p * B);
@@ -904,21 +970,27 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   for (uint32_t bi = 0; bi < nb; bi++) {
     const int b = bi & 1;
     hipStream_t s = ctx->pipe[b];
-    if (bi >= 2) {  // buffer pair b is free once batch bi-2 has landed
+    // Pinned buffer pair b is free once batch bi-2 has landed (device
+    // buffers are reused in stream order and need no host wait).
+    if (bi >= 2 && !(in_direct && (out_direct || p == 0) && !hashes_out)) {
       HIP_TRY(ctx, hipStreamSynchronize(s));
       unpack(bi - 2);
     }
     const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
-    uint8_t *hin = ctx->pipe_in[b].p;
-    if (packed) {
-      pool.copy(hin, data + static_cast<size_t>(c0) * chunk_len, per * cn);
+    const uint8_t *hin = in_direct ? data + static_cast<size_t>(c0) * chunk_len
+                                   : ctx->pipe_in[b].p;
+    if (in_direct) {
+      // the H2D below reads the caller's page-locked chunks in place
+    } else if (packed) {
+      pool.copy(ctx->pipe_in[b].p, data + static_cast<size_t>(c0) * chunk_len, per * cn);
     } else {
       pool.run(static_cast<int>(cn), [&](int c) {
         const uint8_t *src = data + (static_cast<size_t>(c0) + c) * chunk_len;
         for (uint32_t j = 0; j < k; j++) {
           const size_t off = static_cast<size_t>(j) * B;
           const size_t cnt = off < chunk_len ? std::min(B, chunk_len - off) : 0;
-          uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(j) * S;
+          uint8_t *dst = ctx->pipe_in[b].p + static_cast<size_t>(c) * per +
+                         static_cast<size_t>(j) * S;
           if (cnt) std::memcpy(dst, src + off, cnt);
           std::memset(dst + cnt, 0, S - cnt);
         }
@@ -947,7 +1019,9 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                                          s));
     }
     if (back)
-      HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dp, back, hipMemcpyDeviceToHost, s));
+      HIP_TRY(ctx, hipMemcpyAsync(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
+                                             : ctx->pipe_out[b].p,
+                                  dp, back, hipMemcpyDeviceToHost, s));
     if (hashes_out)
       HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch, dh,
                                   static_cast<size_t>(cn) * n * 32, hipMemcpyDeviceToHost, s));

@@ -119,6 +119,32 @@ def test_host_encode_chunks_pipeline(ctx):
             assert np.array_equal(par[c], want), (k, n, L, c)
 
 
+def test_host_encode_chunks_pinned_direct(ctx):
+    """Caller buffers from storb_rs_host_alloc are DMA'd in place; every mix
+    of pinned / pageable input and output gives the oracle's parity."""
+    for k, n, L, cnt in [(4, 6, 1 << 20, 150), (16, 24, 8 << 20, 10), (4, 6, 4096, 7)]:
+        B = -(-L // k)
+        src = _lib.PinnedBuffer(L * cnt)
+        dst = _lib.PinnedBuffer(cnt * (n - k) * B)
+        src.array[:] = rnd(L * cnt, 5 * L + cnt)
+        assert _lib.host_is_pinned(src.array) and _lib.host_is_pinned(dst.array)
+        want = np.concatenate([oracle_parity(k, n, src.array[c * L:(c + 1) * L])[0].reshape(-1)
+                               for c in range(cnt)])
+        pageable_in = src.array.copy()
+        assert not _lib.host_is_pinned(pageable_in)
+        for inp in (src.array, pageable_in):
+            for out in (dst.array, None):
+                if out is not None:
+                    out[:] = 0
+                got = ctx.encode_chunks(k, n, inp, L, cnt, out=out)
+                assert np.array_equal(got[:want.size], want), (k, n, L, out is None)
+        par, hashes = ctx.encode_chunks_hashed(k, n, src.array, L, cnt)
+        assert np.array_equal(par, want)
+        assert bytes(hashes[0, k]) == _lib.blake3(want[:B])
+        src.free()
+        dst.free()
+
+
 # ----------------------------------------------------------- device API
 def dev_encode_check(ctx, k, n, B, ns, kernel=_lib.KERNEL_PERM, offset=0):
     ctx.set_kernel(kernel)
