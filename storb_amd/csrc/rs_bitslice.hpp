@@ -160,7 +160,14 @@ __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 __device__ __forceinline__ v4 ld_nt(const v4 *p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ void st_nt(v4 *p, v4 v) { __builtin_nontemporal_store(v, p); }
+// Stores: default write-back policy unless STORB_RS_NT_STORES (rs_device.hpp).
+__device__ __forceinline__ void st_nt(v4 *p, v4 v) {
+#if STORB_RS_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 
 // One share's 32 bytes (already bit-sliced) folded into the R x 8
 // accumulator planes with the Four-Russians tables.

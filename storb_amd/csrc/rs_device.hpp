@@ -78,13 +78,21 @@ __device__ __forceinline__ uint32_t gf_madd_perm(uint32_t acc, const PermTab &t,
 }
 
 // Shards are streamed exactly once: non-temporal loads and stores keep them
-// from churning L2/MALL (measured +8-10 % on RS(4,2), tools/kbench.hip,
-// reaching the copy ceiling of the same access shape).
+// from churning L2/MALL. Measured back to back (tools/kbench_tune.hip built
+// with STORB_RS_NT_STORES=0/1, profiles/r1_store_policy.txt): nt stores
+// 6.51 vs 6.19 TB/s on RS(4,2) encode, 6.60 vs 6.12 on RS(8,4) decode, 5.87
+// vs 5.38 for the bit-sliced RS(16,8) encoder. (A single-launch timing
+// favours default stores, tools/hbm_probe.hip, because dirty lines left in
+// L2/MALL at kernel end are written back after the end event.)
 __device__ __forceinline__ u32x4 ld_stream(const u32x4 *p) {
   return __builtin_nontemporal_load(p);
 }
 __device__ __forceinline__ void st_stream(u32x4 *p, u32x4 v) {
+#if STORB_RS_NT_STORES
   __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
 }
 
 // Inputs are consumed in groups of up to 8 shares; the next group's

@@ -7,6 +7,13 @@
 
 #include "gf256.hpp"
 
+// Store policy of the shard kernels (rs_device.hpp, rs_bitslice.hpp): 1 =
+// non-temporal stores (measured fastest in steady state), 0 = default
+// write-back stores (kept for the comparison in tools/kbench_tune.hip).
+#ifndef STORB_RS_NT_STORES
+#define STORB_RS_NT_STORES 1
+#endif
+
 namespace storb_rs {
 
 // One launch applies a (r x k) coefficient block to k input share slots and
