@@ -184,7 +184,7 @@ def copy_ceiling(ctx, dev, stream, nbytes=1 << 30, reps=5):
     return rates
 
 
-def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3):
+def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
     """PCIe-inclusive encode: host bytes in, parity out (pipelined). Two
     figures: from pageable caller memory (staged through the context's pinned
     buffers by host copy threads) and from page-locked caller memory
@@ -207,13 +207,32 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3):
             ctx.encode_chunks(k, n, host, chunk_bytes, nchunks, out=out)
         el = time.perf_counter() - t0
         res[mode] = round(reps * nchunks * chunk_bytes / GIB / el, 3)
+        if mode == "pageable" and erased:
+            # download side: every chunk lost `erased`, rebuilt from the first
+            # k survivors (storb_rs_decode_chunks), host shares in, chunks out
+            surv = [i for i in range(n) if i not in erased][:k]
+            par = out.reshape(nchunks, n - k, B)
+            dat = host.reshape(nchunks, k, B)
+            chunks = [([dat[c, i] if i < k else par[c, i - k] for i in surv], surv)
+                      for c in range(nchunks)]
+            rec = np.empty((nchunks, chunk_bytes), np.uint8)
+            ctx.decode_chunks(k, n, B, 0, chunks, out=rec)  # warm
+            if not np.array_equal(rec.reshape(-1), host):
+                raise SystemExit("host decode_chunks round trip mismatch")
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.decode_chunks(k, n, B, 0, chunks, out=rec)
+            res["decode"] = round(reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0), 3)
         if mode == "pinned":
             src.free()
             dst.free()
     return {"value": res["pageable"], "unit": "GiB/s", "pinned_value": res["pinned"],
+            "decode_value": res.get("decode"),
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB host chunks "
                     "-> H2D -> encode -> D2H parity, 2 streams; value = pageable caller "
-                    "buffers (staged), pinned_value = page-locked caller buffers (direct DMA)"}
+                    "buffers (staged), pinned_value = page-locked caller buffers (direct DMA); "
+                    f"decode_value = storb_rs_decode_chunks of the same chunks with shares "
+                    f"{sorted(erased)} lost (host shares in, chunks out)"}
 
 
 def shard_hash_rate(ctx, w, stream, reps=3):
@@ -480,7 +499,8 @@ def main():
                                                                    set(w.erased))
         if not a.no_host_path and a.config in (2, 5):
             out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
-                                                   nchunks=max(8, (256 << 20) // w.chunk))
+                                                   nchunks=max(8, (256 << 20) // w.chunk),
+                                                   erased=[e for e in w.erased if e < w.k])
         if a.config in (2, 5):
             out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
     if rank == 0:

@@ -116,6 +116,21 @@ int storb_rs_encode_chunks_hashed(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                                   uint32_t nchunks, uint8_t *parity_out,
                                   uint8_t *hashes_out);
 
+/* Pipelined host batch decode, the download side (download.rs:453-465
+ * reconstructs one chunk after another): nchunks chunks of one (k, n, block,
+ * padlen), e.g. an object's full-size chunks. Chunk c offers nshares[c]
+ * shares: shares[o_c + i] is share share_idx[o_c + i], o_c = nshares[0] +
+ * ... + nshares[c-1]. Per chunk the first k by index are used (decode_chunk,
+ * piece.rs:368-381); its k*block - padlen bytes land at out + c*out_stride
+ * (out_stride 0 = packed). ENOTENOUGH if any chunk has fewer than k
+ * distinct shares (reconstruct_chunk's Err, piece.rs:462-473); nothing is
+ * guaranteed written then. */
+int storb_rs_decode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                           size_t block, size_t padlen, uint32_t nchunks,
+                           const uint8_t *const *shares,
+                           const uint32_t *share_idx, const uint32_t *nshares,
+                           uint8_t *out, size_t out_stride);
+
 /* ---- page-locked host memory ------------------------------------------ */
 /* Storb fills a chunk buffer from the upload body (upload.rs:333-383) and
  * hands it to encode_chunk (upload.rs:420). When that buffer -- and the

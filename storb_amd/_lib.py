@@ -87,6 +87,9 @@ def _declare(L):
     L.storb_blake3.argtypes = [vp, sz, vp]
     L.storb_blake3.restype = None
     L.storb_rs_blake3_batch_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, vp, vp]
+    L.storb_rs_decode_chunks.argtypes = [vp, C.c_uint32, C.c_uint32, sz, sz, C.c_uint32,
+                                         C.POINTER(vp), C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint32), vp, sz]
     L.storb_rs_host_alloc.argtypes = [sz, C.POINTER(vp)]
     L.storb_rs_host_free.argtypes = [vp]
     L.storb_rs_host_register.argtypes = [vp, sz]
@@ -300,6 +303,34 @@ class Context:
                                                  nchunks, par.ctypes.data, hashes.ctypes.data)
         self._check(rc, "storb_rs_encode_chunks_hashed")
         return par[:nchunks * (n - k) * B], hashes
+
+    def decode_chunks(self, k: int, n: int, block: int, padlen: int, chunks,
+                      out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Batch of download-side reconstructions: chunks[c] = (shares, idx),
+        shares[i] (block bytes) being share idx[i] of chunk c. Returns
+        [nchunks, k*block - padlen] (decode_chunk per chunk, piece.rs:363-387)."""
+        nch = len(chunks)
+        outlen = k * block - padlen
+        if out is None:
+            out = np.empty((nch, outlen), dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= nch * outlen
+        keep, ptrs, idx, cnt = [], [], [], []
+        for shares, ids in chunks:
+            assert len(shares) == len(ids)
+            cnt.append(len(ids))
+            idx.extend(int(i) for i in ids)
+            for sh in shares:
+                a = _as_u8(sh)
+                assert a.size >= block
+                keep.append(a)
+                ptrs.append(a.ctypes.data)
+        P = (vp * max(1, len(ptrs)))(*ptrs)
+        I = (C.c_uint32 * max(1, len(idx)))(*idx)
+        N = (C.c_uint32 * max(1, nch))(*cnt)
+        rc = lib().storb_rs_decode_chunks(self._h, k, n, block, padlen, nch, P, I, N,
+                                          out.ctypes.data, outlen)
+        self._check(rc, "storb_rs_decode_chunks")
+        return out.reshape(-1)[:nch * outlen].reshape(nch, outlen)
 
     # --------------------------------------------------- device buffers
     def encode_batch_dev(self, k: int, n: int, block: int, nstripes: int, d_data: int,

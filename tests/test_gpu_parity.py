@@ -145,6 +145,38 @@ def test_host_encode_chunks_pinned_direct(ctx):
         dst.free()
 
 
+def test_host_decode_chunks_batch(ctx):
+    """Batched download-side decode: every chunk its own survivor set
+    (all-data, data+parity mixes, parity-only, extra shares beyond k, any
+    order); each chunk must equal the original bytes (decode_chunk's first-k
+    rule), including the truncated tail of the padding."""
+    rng = random.Random(11)
+    for k, n, L, cnt in [(4, 6, (1 << 20) - 5, 40), (8, 12, 256 << 10, 25), (16, 24, 777777, 9),
+                         (2, 3, 4096, 12), (1, 2, 100, 5)]:
+        data = rnd(L * cnt, 3 * L + k)
+        chunks, want = [], []
+        for c in range(cnt):
+            chunk = data[c * L:(c + 1) * L]
+            shares, B, pad = coracle.encode(k, n, chunk)
+            m = rng.randint(k, n)
+            ids = rng.sample(range(n), m)
+            if c % 7 == 0:
+                ids = list(range(k))                       # nothing erased
+            elif c % 7 == 1 and n - k >= 1:
+                ids = list(range(n - 1, n - 1 - min(n, k + 1), -1))  # parity first
+            chunks.append(([shares[i] for i in ids], ids))
+            want.append(chunk)
+        got = ctx.decode_chunks(k, n, B, pad, chunks)
+        for c in range(cnt):
+            assert np.array_equal(got[c], want[c]), (k, n, L, c, chunks[c][1])
+    # fewer than k shares in one chunk: the whole call reports ENOTENOUGH
+    shares, B, pad = coracle.encode(4, 6, rnd(4096, 1))
+    with pytest.raises(_lib.StorbRsError) as e:
+        ctx.decode_chunks(4, 6, B, pad, [([shares[i] for i in range(4)], [0, 1, 2, 3]),
+                                         ([shares[i] for i in (0, 4, 5)], [0, 4, 5])])
+    assert e.value.code == _lib.ENOTENOUGH
+
+
 # ----------------------------------------------------------- device API
 def dev_encode_check(ctx, k, n, B, ns, kernel=_lib.KERNEL_PERM, offset=0):
     ctx.set_kernel(kernel)
