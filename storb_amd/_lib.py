@@ -261,6 +261,29 @@ class Context:
         self._check(rc, "storb_rs_decode")
         return out[:outlen].tobytes()
 
+    def encode_into(self, k: int, n: int, data: np.ndarray, parity: Sequence[np.ndarray]):
+        """storb_rs_encode into caller-owned parity buffers (n-k arrays of >=
+        B bytes; page-locked ones are written in place by the kernel)."""
+        buf = _as_u8(data)
+        assert len(parity) == n - k
+        ptrs = (vp * max(n - k, 1))(*[p.ctypes.data for p in parity])
+        b, pad = sz(), sz()
+        rc = lib().storb_rs_encode(self._h, k, n, buf.ctypes.data, buf.size, ptrs,
+                                   C.byref(b), C.byref(pad))
+        self._check(rc, "storb_rs_encode")
+        return int(b.value), int(pad.value)
+
+    def decode_into(self, k: int, n: int, shares: Sequence[np.ndarray], idx: Sequence[int],
+                    block: int, padlen: int, out: np.ndarray):
+        """storb_rs_decode into a caller-owned buffer of k*block - padlen bytes."""
+        assert out.dtype == np.uint8 and out.flags.c_contiguous
+        assert out.size >= k * block - padlen
+        ptrs = (vp * max(len(shares), 1))(*[a.ctypes.data for a in shares])
+        ids = (C.c_uint32 * max(len(idx), 1))(*idx)
+        rc = lib().storb_rs_decode(self._h, k, n, ptrs, ids, len(shares), block, padlen,
+                                   out.ctypes.data)
+        self._check(rc, "storb_rs_decode")
+
     def repair(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
                targets: Sequence[int]) -> list[bytes]:
         """Regenerate shares `targets` (data or parity) of one stripe from the

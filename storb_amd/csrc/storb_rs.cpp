@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -32,6 +33,7 @@ using namespace storb_rs;
 namespace {
 
 constexpr size_t kAlign = 16;
+constexpr int kMaxSlices = 8;
 inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct DevBuf {
@@ -136,6 +138,12 @@ struct storb_rs_ctx {
   PinBuf pipe_in[2], pipe_out[2];
   std::map<std::vector<uint8_t>, std::unique_ptr<Tables>> tables;
   std::unique_ptr<HostPool> pool;  // host copy workers, created on first use
+  // Single-call paths whose staged bytes (in + out) are at most this size
+  // run the kernel straight on the pinned staging buffers (zero-copy over
+  // PCIe) instead of DMA in -> kernel -> DMA out: one launch and one sync
+  // instead of three operations. STORB_RS_ZC_MAX, bytes; 0 disables.
+  size_t zc_max = 0;
+  hipEvent_t slice_ev[kMaxSlices] = {};  // sliced single-call pipeline
 };
 
 namespace {
@@ -394,6 +402,55 @@ hipStream_t pick_stream(storb_rs_ctx *, void *s) {
   return reinterpret_cast<hipStream_t>(s);
 }
 
+// Device address of page-locked host memory (the kernels read / write it
+// over PCIe directly on the zero-copy path).
+hipError_t host_dev_ptr(uint8_t *host, uint8_t **dev) {
+  void *d = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&d, host, 0);
+  *dev = static_cast<uint8_t *>(d);
+  return e;
+}
+
+// Single-call pipeline over column slices of one stripe. A chunk's shares
+// are split into q column ranges [off, off+cnt) (16-B multiples); while the
+// kernel works on slice t (zero-copy, over PCIe), the host packs slice t+1
+// into pinned staging and unpacks slice t-1's outputs, so the staging copies
+// of pageable caller buffers overlap the kernel instead of adding to it.
+// q = 1 (small chunks) degenerates to pack -> launch -> sync -> unpack.
+int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)> &pack,
+           const std::function<int(size_t, size_t)> &launch,
+           const std::function<void(size_t, size_t)> &unpack) {
+  int q = static_cast<int>(std::min<size_t>(kMaxSlices, S / (128u << 10)));
+  if (q < 2) q = 1;
+  const size_t slice = round_up((S + q - 1) / q, kAlign);
+  q = static_cast<int>((S + slice - 1) / slice);
+  for (int t = 0; t < q; t++)
+    if (!ctx->slice_ev[t])
+      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->slice_ev[t], hipEventDisableTiming));
+  auto range = [&](int t, size_t &off, size_t &cnt) {
+    off = static_cast<size_t>(t) * slice;
+    cnt = std::min(slice, S - off);
+  };
+  for (int t = 0; t < q; t++) {
+    size_t off, cnt;
+    range(t, off, cnt);
+    pack(off, cnt);
+    const int rc = launch(off, cnt);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->slice_ev[t], ctx->stream));
+    if (t > 0) {
+      HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[t - 1]));
+      range(t - 1, off, cnt);
+      unpack(off, cnt);
+    }
+  }
+  size_t off, cnt;
+  range(q - 1, off, cnt);
+  HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[q - 1]));
+  unpack(off, cnt);
+  return STORB_RS_OK;
+}
+
 }  // namespace
 
 // ======================================================================
@@ -434,6 +491,8 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   if (!g.ok) return STORB_RS_ENODEV;
   auto *c = new storb_rs_ctx();
   c->device = dev;
+  c->zc_max = 64ull << 20;
+  if (const char *e = std::getenv("STORB_RS_ZC_MAX")) c->zc_max = std::strtoull(e, nullptr, 10);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) != hipSuccess) {
@@ -453,6 +512,8 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   for (auto &p : ctx->pipe)
     if (p) (void)hipStreamDestroy(p);
+  for (auto &e : ctx->slice_ev)
+    if (e) (void)hipEventDestroy(e);
   delete ctx;  // frees tables, staging and pinned buffers on ctx->device
 }
 
@@ -776,25 +837,78 @@ int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *da
   const uint32_t p = n - k;
   if (p == 0) return STORB_RS_OK;
   if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  for (uint32_t i = 0; i < p; i++)
+    if (!parity_out[i]) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
   const size_t S = round_up(B, kAlign);
+  const bool zc = static_cast<size_t>(n) * S <= ctx->zc_max;
+  // Page-locked, 16-B aligned caller buffers need no staging at all.
+  auto aligned = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool in_direct = zc && pad == 0 && S == B && aligned(data) && range_pinned(data, len);
+  bool out_direct = zc && S == B;
+  for (uint32_t i = 0; out_direct && i < p; i++)
+    out_direct = aligned(parity_out[i]) && range_pinned(parity_out[i], B);
   DeviceGuard g(ctx->device);
-  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(p) * S));
-  HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(n) * S));
-  // Zero-padded data shares, S-pitched (zfec pads the tail with zeros).
-  uint8_t *hin = ctx->pin_in.p;
-  for (uint32_t j = 0; j < k; j++) {
-    const size_t off = static_cast<size_t>(j) * B;
-    const size_t cnt = off < len ? std::min(B, len - off) : 0;
-    if (cnt) std::memcpy(hin + static_cast<size_t>(j) * S, data + off, cnt);
-    std::memset(hin + static_cast<size_t>(j) * S + cnt, 0, S - cnt);
-  }
+  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(p) * S));
+  if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(n) * S));
+  HostPool &pool = host_pool(ctx);
   hipStream_t s = ctx->stream;
-  uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
-  HIP_TRY(ctx, hipMemcpyAsync(dd, hin, static_cast<size_t>(k) * S, hipMemcpyHostToDevice, s));
   std::vector<const uint8_t *> in(k);
   std::vector<uint8_t *> out(p);
   std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(p, static_cast<size_t>(p) * S);
+  // Zero-padded data shares, S-pitched (zfec pads the tail with zeros):
+  // columns [off, off + cnt) of every share into pinned staging.
+  auto pack = [&](size_t off, size_t cnt) {
+    const int parts = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
+    pool.run(parts, [&](int part) {
+      for (uint32_t j = static_cast<uint32_t>(part); j < k; j += parts) {
+        const size_t src = static_cast<size_t>(j) * B + off;
+        size_t avail = off < B ? std::min(cnt, B - off) : 0;
+        avail = src < len ? std::min(avail, len - src) : 0;
+        uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(j) * S + off;
+        if (avail) std::memcpy(dst, data + src, avail);
+        if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
+      }
+    });
+  };
+  auto unpack = [&](size_t off, size_t cnt) {
+    const size_t c = off < B ? std::min(cnt, B - off) : 0;
+    if (!c) return;
+    const int parts = static_cast<size_t>(p) * c >= (2u << 20) ? static_cast<int>(p) : 1;
+    pool.run(parts, [&](int part) {
+      for (uint32_t i = static_cast<uint32_t>(part); i < p; i += parts)
+        std::memcpy(parity_out[i] + off, ctx->pin_out.p + static_cast<size_t>(i) * S + off, c);
+    });
+  };
+  if (zc) {  // the kernel reads and writes page-locked host memory over PCIe
+    uint8_t *dd, *dp = nullptr;
+    HIP_TRY(ctx, host_dev_ptr(in_direct ? const_cast<uint8_t *>(data) : ctx->pin_in.p, &dd));
+    std::vector<uint8_t *> pd(p);
+    if (out_direct) {
+      for (uint32_t i = 0; i < p; i++) HIP_TRY(ctx, host_dev_ptr(parity_out[i], &pd[i]));
+    } else {
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dp));
+      for (uint32_t i = 0; i < p; i++) pd[i] = dp + static_cast<size_t>(i) * S;
+    }
+    auto launch = [&](size_t off, size_t cnt) {
+      for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S + off;
+      for (uint32_t i = 0; i < p; i++) out[i] = pd[i] + off;
+      return encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), cnt, 1, s);
+    };
+    if (in_direct && out_direct) {  // nothing to overlap
+      const int rc = launch(0, S);
+      if (rc) return rc;
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      return STORB_RS_OK;
+    }
+    return sliced(
+        ctx, S, [&](size_t off, size_t cnt) { if (!in_direct) pack(off, cnt); }, launch,
+        [&](size_t off, size_t cnt) { if (!out_direct) unpack(off, cnt); });
+  }
+  pack(0, S);
+  uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
+  HIP_TRY(ctx, hipMemcpyAsync(dd, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                              hipMemcpyHostToDevice, s));
   for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
   for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
   int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S, 1, s);
@@ -802,8 +916,7 @@ int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *da
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dp, static_cast<size_t>(p) * S,
                               hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
-  for (uint32_t i = 0; i < p; i++)
-    std::memcpy(parity_out[i], ctx->pin_out.p + static_cast<size_t>(i) * S, B);
+  unpack(0, S);
   return STORB_RS_OK;
 }
 
@@ -827,26 +940,100 @@ int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
     const size_t off = static_cast<size_t>(row) * block;
     if (off < outlen) std::memcpy(out + off, src, std::min(block, outlen - off));
   };
-  for (uint32_t s = 0; s < k; s++)
-    if (slot_idx[s] < k) put(s, shares[slot_pos[s]]);
-  if (missing.empty()) return STORB_RS_OK;  // all data shares present
+  HostPool &pool = host_pool(ctx);
+  const int parts = static_cast<size_t>(k) * block >= (1u << 20) ? static_cast<int>(k) : 1;
+  auto put_present = [&] {  // surviving data shares: plain copies into out
+    pool.run(parts, [&](int part) {
+      for (uint32_t s = static_cast<uint32_t>(part); s < k; s += parts)
+        if (slot_idx[s] < k) put(s, shares[slot_pos[s]]);
+    });
+  };
+  if (missing.empty()) {  // all data shares present: concatenation, as zfec
+    put_present();
+    return STORB_RS_OK;
+  }
   const size_t S = round_up(block, kAlign);
   const uint32_t e = static_cast<uint32_t>(missing.size());
+  const bool zc = static_cast<size_t>(k + e) * S <= ctx->zc_max;
+  auto aligned = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  // Page-locked, aligned caller shares / output are used in place.
+  bool in_direct = zc && S == block;
+  for (uint32_t c = 0; in_direct && c < k; c++)
+    in_direct = aligned(shares[slot_pos[c]]) && range_pinned(shares[slot_pos[c]], block);
+  const bool out_direct = zc && S == block && padlen == 0 && aligned(out) &&
+                          range_pinned(out, outlen);
   DeviceGuard g(ctx->device);
-  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(e) * S));
-  HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + e) * S));
-  for (uint32_t c = 0; c < k; c++) {
-    std::memcpy(ctx->pin_in.p + static_cast<size_t>(c) * S, shares[slot_pos[c]], block);
-    std::memset(ctx->pin_in.p + static_cast<size_t>(c) * S + block, 0, S - block);
-  }
+  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(e) * S));
+  if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + e) * S));
+  // columns [off, off + cnt) of row `row` of the chunk (truncated at outlen)
+  auto put_cols = [&](uint32_t row, size_t off, size_t cnt, const uint8_t *src) {
+    const size_t o = static_cast<size_t>(row) * block + off;
+    size_t c = off < block ? std::min(cnt, block - off) : 0;
+    c = o < outlen ? std::min(c, outlen - o) : 0;
+    if (c) std::memcpy(out + o, src, c);
+  };
+  // slot shares into pinned staging; present data shares also into out
+  auto pack = [&](size_t off, size_t cnt) {
+    const int pp = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
+    pool.run(pp, [&](int part) {
+      for (uint32_t c = static_cast<uint32_t>(part); c < k; c += pp) {
+        const uint8_t *src = shares[slot_pos[c]] + off;
+        const size_t avail = off < block ? std::min(cnt, block - off) : 0;
+        if (!in_direct) {
+          uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(c) * S + off;
+          if (avail) std::memcpy(dst, src, avail);
+          if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
+        }
+        if (slot_idx[c] < k) put_cols(c, off, cnt, src);
+      }
+    });
+  };
+  auto unpack = [&](size_t off, size_t cnt) {
+    if (out_direct) return;
+    for (uint32_t r = 0; r < e; r++)
+      put_cols(missing[r], off, cnt, ctx->pin_out.p + static_cast<size_t>(r) * S + off);
+  };
   hipStream_t s = ctx->stream;
-  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
-  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
-                              hipMemcpyHostToDevice, s));
   std::vector<const uint8_t *> in(k);
   std::vector<uint8_t *> o(e);
   std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(e, static_cast<size_t>(e) * S);
+  if (zc) {  // zero-copy: the kernel reads / writes page-locked host memory
+    std::vector<uint8_t *> id(k), od(e);
+    uint8_t *base = nullptr;
+    if (in_direct) {
+      for (uint32_t c = 0; c < k; c++)
+        HIP_TRY(ctx, host_dev_ptr(const_cast<uint8_t *>(shares[slot_pos[c]]), &id[c]));
+    } else {
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &base));
+      for (uint32_t c = 0; c < k; c++) id[c] = base + static_cast<size_t>(c) * S;
+    }
+    if (out_direct) {
+      HIP_TRY(ctx, host_dev_ptr(out, &base));
+      for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(missing[r]) * block;
+    } else {
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &base));
+      for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(r) * S;
+    }
+    auto launch = [&](size_t off, size_t cnt) {
+      for (uint32_t c = 0; c < k; c++) in[c] = id[c] + off;
+      for (uint32_t r = 0; r < e; r++) o[r] = od[r] + off;
+      return apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), cnt, 1,
+                   s);
+    };
+    if (in_direct && out_direct) {
+      rc = launch(0, S);
+      if (rc) return rc;
+      put_present();  // host copies overlap the kernel (disjoint rows of out)
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      return STORB_RS_OK;
+    }
+    return sliced(ctx, S, pack, launch, unpack);
+  }
+  pack(0, S);
+  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
+  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                              hipMemcpyHostToDevice, s));
   for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
   for (uint32_t r = 0; r < e; r++) o[r] = dout + static_cast<size_t>(r) * S;
   rc = apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1, s);
@@ -854,7 +1041,7 @@ int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(e) * S,
                               hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
-  for (uint32_t r = 0; r < e; r++) put(missing[r], ctx->pin_out.p + static_cast<size_t>(r) * S);
+  unpack(0, S);
   return STORB_RS_OK;
 }
 
@@ -882,9 +1069,15 @@ int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
     std::memset(ctx->pin_in.p + static_cast<size_t>(c) * S + block, 0, S - block);
   }
   hipStream_t s = ctx->stream;
+  const bool zc = static_cast<size_t>(k + ntargets) * S <= ctx->zc_max;
   uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
-  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
-                              hipMemcpyHostToDevice, s));
+  if (zc) {  // zero-copy: the kernel works on the pinned staging directly
+    HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &din));
+    HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dout));
+  } else {
+    HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                                hipMemcpyHostToDevice, s));
+  }
   std::vector<const uint8_t *> in(k);
   std::vector<uint8_t *> o(ntargets);
   std::vector<size_t> ins(k, static_cast<size_t>(k) * S),
@@ -894,8 +1087,9 @@ int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
   rc = apply(ctx, k, ntargets, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1,
              s);
   if (rc) return rc;
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(ntargets) * S,
-                              hipMemcpyDeviceToHost, s));
+  if (!zc)
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(ntargets) * S,
+                                hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   for (uint32_t r = 0; r < ntargets; r++)
     std::memcpy(out[r], ctx->pin_out.p + static_cast<size_t>(r) * S, block);

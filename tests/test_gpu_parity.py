@@ -145,6 +145,61 @@ def test_host_encode_chunks_pinned_direct(ctx):
         dst.free()
 
 
+@pytest.mark.parametrize("zc", [True, False])
+def test_single_call_pinned_and_staged(zc, monkeypatch):
+    """storb_rs_encode / storb_rs_decode (the zfec-rs shim's per-chunk
+    calls) on page-locked caller buffers (used in place) and on pageable
+    ones (staged), through the zero-copy kernel path and the DMA path."""
+    monkeypatch.setenv("STORB_RS_ZC_MAX", str(64 << 20) if zc else "0")
+    c = _lib.Context(0)
+    for k, n, B in [(4, 6, 256 << 10), (16, 24, 512 << 10), (1, 2, 65536), (8, 12, 4096)]:
+        L = k * B
+        pin = [_lib.PinnedBuffer(B) for _ in range(n)]     # n shares
+        pout = _lib.PinnedBuffer(L)
+        src = _lib.PinnedBuffer(L)
+        src.array[:] = rnd(L, k + n + B)
+        want = oracle_parity(k, n, src.array)[0]
+        for data in (src.array, src.array.copy()):
+            for par in ([pin[k + i].array for i in range(n - k)],
+                        [np.zeros(B, np.uint8) for _ in range(n - k)]):
+                for p in par:
+                    p[:] = 0
+                assert c.encode_into(k, n, data, par) == (B, 0)
+                assert all(np.array_equal(par[i], want[i]) for i in range(n - k)), (k, n)
+        for i in range(k):
+            pin[i].array[:] = src.array[i * B:(i + 1) * B]
+        for i in range(n - k):
+            pin[k + i].array[:] = want[i]
+        ids = list(range(min(2, n - k), n))[:k]          # lose the first data shares
+        for shares in ([pin[i].array for i in ids], [pin[i].array.copy() for i in ids]):
+            for out in (pout.array, np.empty(L, np.uint8)):
+                out[:] = 0
+                c.decode_into(k, n, shares, ids, B, 0, out)
+                assert np.array_equal(out, src.array), (k, n, ids)
+        for b in pin + [pout, src]:
+            b.free()
+    c.close()
+
+
+@pytest.mark.parametrize("k,n,L", [(4, 6, (3 << 20) + 5), (16, 24, (8 << 20) - 77),
+                                   (3, 5, (1 << 20) + 1), (8, 12, 4 << 20)])
+def test_single_call_large_ragged(ctx, k, n, L):
+    """Chunks big enough for the sliced single-call pipeline (column slices
+    of a share, pack / kernel / unpack overlapped), with ragged lengths so
+    the zero padding and the truncated last row fall inside a slice."""
+    data = rnd(L, L % 1000)
+    par, B, pad = ctx.encode(k, n, data)
+    want, wB, wpad = oracle_parity(k, n, data)
+    assert (B, pad) == (wB, wpad)
+    for i in range(n - k):
+        assert par[i] == want[i].tobytes(), (k, n, L, i)
+    shares = coracle.encode(k, n, data)[0]
+    for lost in ([0], list(range(min(n - k, k))), [k - 1]):
+        ids = [i for i in range(n) if i not in lost][:k]
+        got = ctx.decode(k, n, [shares[i] for i in ids], ids, B, pad)
+        assert got == data.tobytes(), (k, n, L, lost)
+
+
 def test_host_decode_chunks_batch(ctx):
     """Batched download-side decode: every chunk its own survivor set
     (all-data, data+parity mixes, parity-only, extra shares beyond k, any
