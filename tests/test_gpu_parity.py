@@ -473,3 +473,88 @@ def test_config3_full_size_decode_three_erased(ctx):
     want, _, _ = oracle_parity(k, n, coracle.splitmix_bytes(0x5709B + s, L))
     got = par[s * 4 * B:(s + 1) * 4 * B].cpu().numpy().reshape(4, B)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.slow
+def test_config4_round_robin_objects_match_single_batch(ctx):
+    """Config 4: 10,000 x 1 MiB objects, RS(4,2) [storb k=4,m=6]. Each of 8
+    (virtual) ranks encodes only its objects i = rank (mod 8) -- the
+    multi-GPU partition, here on one device -- and every object's parity
+    equals the single-batch encode of all 10,000 (checksum per object and a
+    checksum of checksums), with sampled objects checked against the oracle."""
+    from storb_amd import partition
+
+    k, n, L, N, W = 4, 6, 1 << 20, 10000, 8
+    B = L // k
+    data = torch.empty(N * L, dtype=torch.uint8, device=DEV)
+    ctx.fill_splitmix_dev(data.data_ptr(), L, N, L, 0x5709B)
+    whole = torch.empty(N * 2 * B, dtype=torch.uint8, device=DEV)
+    ctx.encode_batch_dev(k, n, B, N, data.data_ptr(), whole.data_ptr())
+    parts = torch.full_like(whole, 0x5A)
+    for rank in range(W):
+        objs = partition.objects_for_rank(N, rank, W)
+        # objects rank, rank+W, ...: a strided batch (stride W objects)
+        ctx.encode_batch_dev(k, n, B, len(objs), data.data_ptr() + rank * L,
+                             parts.data_ptr() + rank * 2 * B, data_stride=W * L,
+                             parity_stride=W * 2 * B)
+    ctx.sync()
+    cw = whole.view(N, -1).to(torch.int64).sum(dim=1)
+    cp = parts.view(N, -1).to(torch.int64).sum(dim=1)
+    assert torch.equal(cw, cp)
+    assert int(cw.sum()) == int(cp.sum())
+    assert torch.equal(whole, parts)
+    for s in (0, 7, 4999, N - 1):
+        want, _, _ = oracle_parity(k, n, coracle.splitmix_bytes(0x5709B + s, L))
+        assert np.array_equal(whole[s * 2 * B:(s + 1) * 2 * B].cpu().numpy().reshape(2, B), want)
+
+
+@pytest.mark.slow
+def test_config5_full_size_linearity_and_max_erasure(ctx):
+    """Config 5's GPU half: 128 x 8 MiB chunks, storb k=16, m=24 (bit-sliced
+    encoder under AUTO). Size-independent properties: the code is linear
+    (parity(a ^ b) == parity(a) ^ parity(b)), and decoding with all 8 parity
+    shares standing in for data shares 0..7 (the most erasures) returns the
+    data; one stripe is compared with the oracle byte for byte."""
+    k, n, L, N = 16, 24, 8 << 20, 128
+    B = L // k
+    a = torch.empty(N * L, dtype=torch.uint8, device=DEV)
+    b = torch.empty_like(a)
+    ctx.fill_splitmix_dev(a.data_ptr(), L, N, L, 1)
+    ctx.fill_splitmix_dev(b.data_ptr(), L, N, L, 0x5709B)
+    c = a ^ b
+    pars = []
+    for x in (a, b, c):
+        p = torch.empty(N * 8 * B, dtype=torch.uint8, device=DEV)
+        ctx.encode_batch_dev(k, n, B, N, x.data_ptr(), p.data_ptr())
+        pars.append(p)
+    ctx.sync()
+    assert torch.equal(pars[0] ^ pars[1], pars[2])
+    ref = a.clone()
+    a.view(N, k, B)[:, :8].fill_(0xA5)
+    ctx.decode_batch_dev(k, n, B, N, list(range(8, 24)), a.data_ptr(), pars[0].data_ptr(),
+                         a.data_ptr())
+    ctx.sync()
+    assert torch.equal(a, ref)
+    want, _, _ = oracle_parity(k, n, coracle.splitmix_bytes(1 + 77, L))
+    assert np.array_equal(pars[0][77 * 8 * B:78 * 8 * B].cpu().numpy().reshape(8, B), want)
+
+
+@pytest.mark.parametrize("k,n,erased", [(1, 256, (0,)), (255, 256, (0,)),
+                                        (128, 256, tuple(range(0, 128, 1)))])
+def test_max_share_count_roundtrip(ctx, k, n, erased):
+    """zfec's limit n = 256 (the most shares a GF(2^8) code has): encode
+    against the oracle, then decode with `erased` data shares lost (k = 128
+    with all 128 data shares rebuilt from parity: a 128 x 128 inverse tiled
+    over 16 x 32 kernel slots)."""
+    B, ns = 256, 2
+    dev_encode_check(ctx, k, n, B, ns)
+    host = rnd(ns * k * B, n + k)
+    data = to_dev(host)
+    par = torch.zeros(ns * (n - k) * B, dtype=torch.uint8, device=DEV)
+    ctx.set_kernel(_lib.KERNEL_AUTO)
+    ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
+    surv = [i for i in range(n) if i not in erased]
+    data.view(ns, k, B)[:, list(erased)] = 0
+    ctx.decode_batch_dev(k, n, B, ns, surv, data.data_ptr(), par.data_ptr(), data.data_ptr())
+    ctx.sync()
+    assert np.array_equal(data.cpu().numpy(), host)
