@@ -360,7 +360,7 @@ inline uint64_t tile_blocks(const ApplyArgs &a) {
 template <int KM, int RM>
 hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
   using C = Tune<KM, RM>;
-  return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL>(a, s);
+  return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s);
 }
 
 template <int KM>
