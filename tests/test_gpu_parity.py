@@ -558,3 +558,4 @@ def test_max_share_count_roundtrip(ctx, k, n, erased):
     ctx.decode_batch_dev(k, n, B, ns, surv, data.data_ptr(), par.data_ptr(), data.data_ptr())
     ctx.sync()
     assert np.array_equal(data.cpu().numpy(), host)
+
