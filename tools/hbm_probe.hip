@@ -172,6 +172,35 @@ __global__ void fill_random(uint32_t *p, uint64_t n) {
   }
 }
 
+// RS(4,2) traffic with the workgroup -> tile map made XCD-aware: the
+// dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b
+// runs on XCD b % 8; remapped, XCD x streams the contiguous x-th eighth of
+// the tiles (tile = (b % 8) * (grid / 8) + b / 8) instead of every 8th tile.
+template <bool NTS, int T>
+__global__ __launch_bounds__(T) void probe_xcd(const Args a) {
+  const uint32_t cols = static_cast<uint32_t>(a.B >> 4);
+  const uint32_t tps = cols / T;
+  const uint32_t per = gridDim.x / 8;
+  const uint32_t bid = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  const uint32_t stripe = bid / tps, tile = bid % tps;
+  const uint32_t c = tile * T + threadIdx.x;
+  const u32x4 *in = reinterpret_cast<const u32x4 *>(a.in + static_cast<uint64_t>(stripe) * 4 * a.B);
+  u32x4 *out = reinterpret_cast<u32x4 *>(a.out + static_cast<uint64_t>(stripe) * 2 * a.B);
+  u32x4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) v[j] = __builtin_nontemporal_load(in + j * cols + c);
+  u32x4 acc = v[0] ^ v[1] ^ v[2] ^ v[3];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    u32x4 o = acc;
+    o.x ^= i;
+    if (NTS)
+      __builtin_nontemporal_store(o, out + i * cols + c);
+    else
+      out[i * cols + c] = o;
+  }
+}
+
 struct Variant {
   std::string name;
   double bytes;
@@ -269,6 +298,17 @@ int main(int argc, char **argv) {
   ADDW(16, false, 1);
   ADDW(8, true, 2);
   ADDW(8, false, 2);
+
+  vs.push_back(Variant{"xcd-remapped KI=4 RO=2 nt/nt", static_cast<double>(NS) * 6 * B,
+                       [=](hipStream_t s) {
+                         hipLaunchKernelGGL((probe_xcd<true, T>), dim3(grid), dim3(T), 0, s, a);
+                       },
+                       {}});
+  vs.push_back(Variant{"xcd-remapped KI=4 RO=2 nt/default", static_cast<double>(NS) * 6 * B,
+                       [=](hipStream_t s) {
+                         hipLaunchKernelGGL((probe_xcd<false, T>), dim3(grid), dim3(T), 0, s, a);
+                       },
+                       {}});
 
   hipStream_t s;
   CK(hipStreamCreate(&s));
