@@ -14,7 +14,7 @@ reconstructs with decode_chunk's rule (sort, first k) on the GPU
 chain, network-fetched crsqlite, >100-chunk channel hang,
 download.rs:26,500) -- see SURVEY.md fact 9.
 
-usage: python tools/loopback.py [--size BYTES] [--miners N] [--json]
+usage: python tools/loopback.py [--size BYTES] [--miners N]   (prints one JSON line)
        python tools/loopback.py miner --store-port P --http-port Q --dir D
 """
 from __future__ import annotations
@@ -246,15 +246,29 @@ def _run(a, miners):
     out = np.empty(a.size, dtype=np.uint8)
     needed_parity = 0
     t2 = time.perf_counter()
-    for ci, meta in enumerate(metas):
-        got = gathered[ci]
-        if len(got) < meta["k"]:
-            raise SystemExit(f"chunk {ci}: not enough pieces ({len(got)} < {meta['k']})")
-        idx = sorted(got)[:meta["k"]]  # decode_chunk: sort, first k
-        needed_parity += any(i >= meta["k"] for i in idx)
-        rec = ctx.decode(meta["k"], meta["m"], [got[i] for i in idx], idx, meta["B"],
-                         meta["padlen"])
-        out[meta["off"]:meta["off"] + meta["len"]] = np.frombuffer(rec, dtype=np.uint8)
+    # Consecutive chunks of one geometry (all but a short tail) reconstruct in
+    # one storb_rs_decode_chunks call straight into the object buffer; each
+    # chunk keeps decode_chunk's own first-k-by-index choice.
+    runs, ci = [], 0
+    while ci < len(metas):
+        geo = tuple(metas[ci][x] for x in ("k", "m", "B", "padlen", "len"))
+        cj = ci
+        while cj < len(metas) and tuple(metas[cj][x] for x in ("k", "m", "B", "padlen", "len")) == geo:
+            cj += 1
+        runs.append((ci, cj))
+        ci = cj
+    for c0, c1 in runs:
+        meta = metas[c0]
+        batch = []
+        for ci in range(c0, c1):
+            got = gathered[ci]
+            if len(got) < meta["k"]:
+                raise SystemExit(f"chunk {ci}: not enough pieces ({len(got)} < {meta['k']})")
+            ids = sorted(got)
+            needed_parity += any(i >= meta["k"] for i in ids[:meta["k"]])
+            batch.append(([got[i] for i in ids], ids))
+        view = out[meta["off"]:meta["off"] + (c1 - c0) * meta["len"]].reshape(c1 - c0, meta["len"])
+        ctx.decode_chunks(meta["k"], meta["m"], meta["B"], meta["padlen"], batch, out=view)
     t_decode = time.perf_counter() - t2
     t_download = time.perf_counter() - t1
     ok = bool(np.array_equal(out, obj))
