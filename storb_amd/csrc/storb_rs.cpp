@@ -143,6 +143,9 @@ struct storb_rs_ctx {
   // PCIe) instead of DMA in -> kernel -> DMA out: one launch and one sync
   // instead of three operations. STORB_RS_ZC_MAX, bytes; 0 disables.
   size_t zc_max = 0;
+  // storb_rs_encode_chunks without piece ids: zero-copy kernels (1) or
+  // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
+  bool zc_batch = true;
   hipEvent_t slice_ev[kMaxSlices] = {};  // sliced single-call pipeline
 };
 
@@ -493,6 +496,7 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   c->device = dev;
   c->zc_max = 64ull << 20;
   if (const char *e = std::getenv("STORB_RS_ZC_MAX")) c->zc_max = std::strtoull(e, nullptr, 10);
+  if (const char *e = std::getenv("STORB_RS_ZC_BATCH")) c->zc_batch = std::atoi(e) != 0;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) != hipSuccess) {
@@ -1126,11 +1130,20 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   const bool in_direct = packed && range_pinned(data, static_cast<size_t>(nchunks) * chunk_len);
   const bool out_direct =
       p > 0 && S == B && range_pinned(parity_out, static_cast<size_t>(nchunks) * p * B);
+  // Page-locked caller chunks without piece ids: the kernel reads them (and
+  // writes parity) over PCIe directly (zero-copy). Kernel-driven PCIe
+  // traffic overlaps both directions, where the SDMA copies of H2D and D2H
+  // share one ceiling (57 GB/s total, tools/pcie_probe.py): 47 vs 35 GiB/s
+  // measured. From pageable chunks the SDMA pipeline stays ahead (34 vs
+  // 20 GiB/s: the host's packing competes with the kernel's reads of the
+  // same staging), and the hashed path keeps the shares on the device.
+  const bool zc = ctx->zc_batch && !hashes_out && p > 0 && in_direct;
   DeviceGuard g(ctx->device);
   for (int b = 0; b < 2; b++) {
     if (!in_direct) HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
     HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch + hash_bytes));
-    HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
+    if (!zc)
+      HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
   }
   const uint32_t nb = (nchunks + batch - 1) / batch;
   HostPool &pool = host_pool(ctx);
@@ -1189,6 +1202,22 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
           std::memset(dst + cnt, 0, S - cnt);
         }
       });
+    }
+    if (zc) {  // the kernel reads the pinned chunks and writes pinned parity over PCIe
+      uint8_t *di, *dq;
+      HIP_TRY(ctx, host_dev_ptr(const_cast<uint8_t *>(hin), &di));
+      HIP_TRY(ctx, host_dev_ptr(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
+                                           : ctx->pipe_out[b].p,
+                                &dq));
+      std::vector<const uint8_t *> in(k);
+      std::vector<uint8_t *> out(p);
+      std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
+      for (uint32_t j = 0; j < k; j++) in[j] = di + static_cast<size_t>(j) * S;
+      for (uint32_t i = 0; i < p; i++) out[i] = dq + static_cast<size_t>(i) * S;
+      const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S,
+                                  cn, s);
+      if (rc) return rc;
+      continue;
     }
     uint8_t *dd = ctx->pipe_dev[b].p;
     uint8_t *dp = dd + per * batch;
