@@ -207,6 +207,15 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
             ctx.encode_chunks(k, n, host, chunk_bytes, nchunks, out=out)
         el = time.perf_counter() - t0
         res[mode] = round(reps * nchunks * chunk_bytes / GIB / el, 3)
+        if mode == "pageable":
+            # upload path with Storb's piece ids (upload.rs:623) hashed on the GPU
+            ids = np.zeros((nchunks, n, 32), np.uint8)
+            ctx.encode_chunks_hashed(k, n, host, chunk_bytes, nchunks, out=out, hashes=ids)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.encode_chunks_hashed(k, n, host, chunk_bytes, nchunks, out=out, hashes=ids)
+            res["hashed"] = round(reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0),
+                                  3)
         if mode == "pageable" and erased:
             # download side: every chunk lost `erased`, rebuilt from the first
             # k survivors (storb_rs_decode_chunks), host shares in, chunks out
@@ -227,10 +236,12 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
             src.free()
             dst.free()
     return {"value": res["pageable"], "unit": "GiB/s", "pinned_value": res["pinned"],
-            "decode_value": res.get("decode"),
+            "decode_value": res.get("decode"), "hashed_value": res.get("hashed"),
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB host chunks "
                     "-> H2D -> encode -> D2H parity, 2 streams; value = pageable caller "
-                    "buffers (staged), pinned_value = page-locked caller buffers (direct DMA); "
+                    "buffers (staged), pinned_value = page-locked caller buffers (zero-copy kernels); "
+                    "hashed_value = storb_rs_encode_chunks_hashed (parity + every share's blake3 "
+                    "id computed on the GPU), pageable; "
                     f"decode_value = storb_rs_decode_chunks of the same chunks with shares "
                     f"{sorted(erased)} lost (host shares in, chunks out)"}
 

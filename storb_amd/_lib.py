@@ -314,14 +314,20 @@ class Context:
         return out
 
     def encode_chunks_hashed(self, k: int, n: int, data: np.ndarray, chunk_len: int,
-                             nchunks: int):
+                             nchunks: int, out: Optional[np.ndarray] = None,
+                             hashes: Optional[np.ndarray] = None):
         """(parity [nchunks*(n-k)*B], digests [nchunks, n, 32]) -- piece ids
-        computed on the GPU."""
+        computed on the GPU. `out` / `hashes` reuse caller buffers."""
         buf = _as_u8(data)
         assert buf.size >= chunk_len * nchunks
         B = block_size(k, chunk_len)
-        par = np.empty(max(1, nchunks * (n - k) * B), dtype=np.uint8)
-        hashes = np.empty((nchunks, n, 32), dtype=np.uint8)
+        par = out if out is not None else np.empty(max(1, nchunks * (n - k) * B), np.uint8)
+        assert par.dtype == np.uint8 and par.flags.c_contiguous
+        assert par.size >= nchunks * (n - k) * B
+        if hashes is None:
+            hashes = np.empty((nchunks, n, 32), dtype=np.uint8)
+        assert hashes.dtype == np.uint8 and hashes.flags.c_contiguous
+        assert hashes.size >= nchunks * n * 32
         rc = lib().storb_rs_encode_chunks_hashed(self._h, k, n, buf.ctypes.data, chunk_len,
                                                  nchunks, par.ctypes.data, hashes.ctypes.data)
         self._check(rc, "storb_rs_encode_chunks_hashed")
