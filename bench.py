@@ -272,6 +272,36 @@ def shard_hash_rate(ctx, w, stream, reps=3):
             "what": "blake3 (Storb piece id) of all data+parity shards, batched kernel"}
 
 
+def repair_rate(ctx, w, stream, reps=5):
+    """Decode-based repair (repair.rs:44-277 today re-fetches a
+    replica): regenerate one lost share of every stripe in place from the
+    first k survivors. Two cases: a lost data share and a lost parity share.
+    Algorithmic bytes per stripe: k*B read + 1*B written."""
+    k, n, B, N = w.k, w.n, w.B, w.N
+    sp = stream.cuda_stream
+    res = {}
+    for name, lost in (("data", 0), ("parity", n - 1)):
+        surv = [i for i in range(n) if i != lost][:k]
+
+        def go():
+            ctx.repair_batch_dev(k, n, B, N, surv, [lost], w.dptr, w.pptr, stream=sp)
+
+        go()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            go()
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        gbs = N * (k + 1) * B / (ms * 1e-3) / 1e9
+        res[name] = {"lost_share": lost, "ms": round(ms, 4), "GBps": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    res["what"] = (f"storb_rs_repair_batch_dev: {N} stripes, one lost share each rebuilt in "
+                   f"place from the first {k} survivors; bytes = k*B read + B written")
+    return res
+
+
 def kernel_names(kernel, w):
     """The kernels the legs launch (rs_bitslice.hpp / rs_device.hpp)."""
     names = {}
@@ -514,6 +544,7 @@ def main():
                                                    erased=[e for e in w.erased if e < w.k])
         if a.config in (2, 5):
             out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
+            out["repair"] = repair_rate(ctx, w, stream)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
