@@ -559,3 +559,43 @@ def test_max_share_count_roundtrip(ctx, k, n, erased):
     ctx.sync()
     assert np.array_equal(data.cpu().numpy(), host)
 
+
+
+def test_concurrent_calls_per_thread_and_shared_context():
+    """The shim's threading model (one context per tokio worker thread,
+    INTEGRATION.md) and a context shared by several threads (calls serialise
+    on its mutex): 8 threads mixing single-chunk encodes and decodes of
+    several Storb geometries, bit-exact against the oracle."""
+    import threading
+
+    shared = _lib.Context(0)
+    geos = [(4, 6, 1 << 20), (2, 3, 256 << 10), (1, 2, 65536), (16, 24, (3 << 20) + 7),
+            (8, 12, 777)]
+    errors = []
+
+    def worker(t):
+        ctx = _lib.Context(0) if t % 2 == 0 else shared
+        rng = random.Random(t)
+        try:
+            for it in range(10):
+                k, n, L = geos[(t + it) % len(geos)]
+                data = rnd(L, 77 * t + it)
+                par, B, pad = ctx.encode(k, n, data)
+                want = oracle_parity(k, n, data)[0]
+                assert all(par[i] == want[i].tobytes() for i in range(n - k)), (t, k, n, L)
+                shares = coracle.encode(k, n, data)[0]
+                ids = rng.sample(range(n), k)
+                assert ctx.decode(k, n, [shares[i] for i in ids], ids, B, pad) == data.tobytes()
+        except Exception as e:
+            errors.append(f"thread {t}: {e!r}")
+        finally:
+            if ctx is not shared:
+                ctx.close()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    shared.close()
+    assert not errors, errors[:3]
