@@ -56,6 +56,7 @@ struct W {
   uint64_t B;
   std::vector<V> vs;
   bool inplace = false;  // decode layout of bench --config 3 (see below)
+  int order = 0;  // survivor order: 0 index, 1 library slot order (parity in the holes), 2 parity first
 };
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL = false, bool PAIR = false>
@@ -100,13 +101,19 @@ int main(int argc, char **argv) {
                        {"W2 RS(8,4) decode e=3 4096 x 256 KiB", 8, 3, 4096, 32 << 10, {}},
                        {"W3 RS(16,8) encode 128 x 8 MiB", 16, 8, 128, 512 << 10, {}},
                        {"W2i RS(8,4) decode e=3 in place (bench config 3 layout)", 8, 3, 4096,
-                        32 << 10, {}, true}};
+                        32 << 10, {}, true},
+                       {"W2s RS(8,4) decode e=3 in place, survivors in the library's slot order",
+                        8, 3, 4096, 32 << 10, {}, true, 1},
+                       {"W2p RS(8,4) decode e=3 in place, parity survivors first",
+                        8, 3, 4096, 32 << 10, {}, true, 2}};
   add_all<4, 2>(ws[0].vs);
   add_all<8, 3>(ws[1].vs);
   add_all<16, 8>(ws[2].vs);
   add_all<8, 3>(ws[3].vs);
   ws[3].vs.push_back(mk<8, 4, 256, 1, false, 8, true>());  // previous pow2 bucket
   ws[3].vs.back().name += " (r padded to 4)";
+  ws[4].vs.push_back(product<8, 3>());
+  ws[5].vs.push_back(product<8, 3>());
   if (argc > 2) ws.erase(ws.begin(), ws.begin() + std::atoi(argv[2]));
   hipStream_t s;
   CK(hipStreamCreate(&s));
@@ -148,7 +155,12 @@ int main(int argc, char **argv) {
       // survivors {1,2,4,6,7} from the data region (stride 8B) and parity
       // {8,9,10} from the parity region (stride 4B); rebuilt {0,3,5} written
       // into the data region: exactly decode_batch_dev(..., d_out = d_data).
-      const int surv[8] = {1, 2, 4, 6, 7, 8, 9, 10}, lost[3] = {0, 3, 5};
+      // index order, or storb_rs.cpp select_shares' slot order: data share s
+      // in slot s, parity shares filling the holes {0, 3, 5}
+      const int orders[3][8] = {{1, 2, 4, 6, 7, 8, 9, 10}, {8, 1, 2, 9, 4, 10, 6, 7},
+                                {8, 9, 10, 1, 2, 4, 6, 7}};
+      const int *surv = orders[w.order];
+      const int lost[3] = {0, 3, 5};
       for (int j = 0; j < 8; j++) {
         a.in[j] = surv[j] < 8 ? in + surv[j] * w.B : out + (surv[j] - 8) * w.B;
         a.in_stride[j] = surv[j] < 8 ? 8 * w.B : 4 * w.B;
