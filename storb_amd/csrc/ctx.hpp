@@ -1,0 +1,180 @@
+// ctx.hpp -- internals shared by the host-side translation units of the C
+// ABI: the context (streams, staging, table cache), error plumbing, and the
+// helpers behind every entry point.
+//
+//   storb_rs.cpp    context lifecycle, parameters, coefficient tables and the
+//                   (rows x k) apply, device-resident batched calls, blake3,
+//                   page-locked host registry
+//   host_calls.cpp  single-chunk host calls (zfec-rs Fec::encode / decode,
+//                   repair): zero-copy and column-sliced paths
+//   host_batch.cpp  pipelined host batches (encode_chunks[_hashed],
+//                   decode_chunks)
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/storb_rs.h"
+#include "gf256.hpp"
+#include "host_pool.hpp"
+#include "rs_kernels.hpp"
+
+namespace storb_rs {
+namespace detail {
+
+constexpr size_t kAlign = 16;
+constexpr int kMaxSlices = 8;
+inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct DevBuf {
+  uint8_t *p = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), n);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+};
+
+struct PinBuf {
+  uint8_t *p = nullptr;
+  size_t cap = 0;
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+};
+
+// Device-resident coefficient tables for one (rows x k) matrix, tiled in
+// kSlotR x kSlotK blocks: for block b, ptab + b_off[b] PermTabs and
+// btab + b_off[b]*256 product-table bytes.
+struct Tables {
+  uint8_t *dev = nullptr;
+  size_t perm_bytes = 0;
+  std::vector<size_t> b_off;
+  ~Tables() {
+    if (dev) (void)hipFree(dev);
+  }
+};
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace detail
+}  // namespace storb_rs
+
+struct storb_rs_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t pipe[2] = {nullptr, nullptr};
+  int variant = STORB_RS_KERNEL_AUTO;
+  std::mutex mu;
+  std::string last_error;
+  storb_rs::detail::DevBuf stage;
+  storb_rs::detail::DevBuf pipe_dev[2];
+  storb_rs::detail::PinBuf pin_in, pin_out;
+  storb_rs::detail::PinBuf pipe_in[2], pipe_out[2];
+  std::map<std::vector<uint8_t>, std::unique_ptr<storb_rs::detail::Tables>> tables;
+  std::unique_ptr<storb_rs::HostPool> pool;  // host copy workers, created on first use
+  // Single-call paths whose staged bytes (in + out) are at most this size
+  // run the kernel straight on the pinned staging buffers (zero-copy over
+  // PCIe) instead of DMA in -> kernel -> DMA out: one launch and one sync
+  // instead of three operations. STORB_RS_ZC_MAX, bytes; 0 disables.
+  size_t zc_max = 0;
+  // storb_rs_encode_chunks without piece ids: zero-copy kernels (1) or
+  // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
+  bool zc_batch = true;
+  hipEvent_t slice_ev[storb_rs::detail::kMaxSlices] = {};  // sliced single-call pipeline
+};
+
+namespace storb_rs {
+namespace detail {
+
+inline int fail(storb_rs_ctx *ctx, int code, const std::string &msg) {
+  if (ctx) ctx->last_error = msg;
+  return code;
+}
+
+inline int hip_fail(storb_rs_ctx *ctx, hipError_t e, const char *what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(ctx, e == hipErrorOutOfMemory ? STORB_RS_ENOMEM : STORB_RS_EDEVICE, m);
+}
+
+#define HIP_TRY(ctx, expr)                              \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+  } while (0)
+
+// Generator rows of (k, n), built once per geometry.
+const std::vector<uint8_t> &cached_enc(uint32_t k, uint32_t n);
+// Contexts created with device -1 take devices round-robin.
+int next_round_robin();
+// [p, p+len) inside one storb_rs_host_alloc / _register range.
+bool range_pinned(const void *p, size_t len);
+Variant pick_variant(const storb_rs_ctx *ctx);
+// Device tables of a rows x k coefficient matrix (cached per context).
+int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
+               hipStream_t s, const Tables **out);
+// out_r = sum_j coef[r][j] * in_j for every stripe, tiled onto kernel slots.
+int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
+          const uint8_t *const *d_in, const size_t *in_stride, uint8_t *const *d_out,
+          const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s);
+// Parity rows of (k, n): the bit-sliced encoder where compiled in, else apply.
+int encode_apply(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *d_in,
+                 const size_t *in_stride, uint8_t *const *d_out, const size_t *out_stride,
+                 size_t block, uint32_t nstripes, hipStream_t s);
+// decode_chunk's selection (first k by index) and zfec's slot arrangement.
+int select_shares(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint32_t *share_idx,
+                  uint32_t nshares, std::vector<uint32_t> &slot_idx,
+                  std::vector<uint32_t> &slot_pos);
+// Rows of the inverted survivor matrix that rebuild the missing data shares.
+int decode_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                const std::vector<uint32_t> &slot_idx, std::vector<uint8_t> &coef,
+                std::vector<uint32_t> &missing);
+// Rows that regenerate arbitrary target shares (data or parity).
+int repair_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                const std::vector<uint32_t> &slot_idx, const uint32_t *targets,
+                uint32_t ntargets, std::vector<uint8_t> &coef);
+HostPool &host_pool(storb_rs_ctx *ctx);
+hipStream_t pick_stream(storb_rs_ctx *ctx, void *s);
+// Device address of page-locked host memory.
+hipError_t host_dev_ptr(uint8_t *host, uint8_t **dev);
+// Single-call pipeline over column slices of one stripe (host_calls.cpp).
+int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)> &pack,
+           const std::function<int(size_t, size_t)> &launch,
+           const std::function<void(size_t, size_t)> &unpack);
+
+}  // namespace detail
+}  // namespace storb_rs

@@ -1,0 +1,328 @@
+// host_batch.cpp -- pipelined host batches of the C ABI: the chunk loop of
+// upload.rs:418-420 (storb_rs_encode_chunks, with blake3 piece ids:
+// storb_rs_encode_chunks_hashed) and of download.rs:453-465
+// (storb_rs_decode_chunks), double-buffered over two streams.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "ctx.hpp"
+
+using namespace storb_rs;
+using namespace storb_rs::detail;
+
+extern "C" {
+
+// Pipelined batch encode: two pinned in/out buffer pairs and two streams.
+// While the GPU copies and encodes batch i, the host packs batch i+1 and
+// unpacks batch i-1 (hipMemcpyAsync from pinned memory is a true DMA).
+// With hashes_out, the blake3 of every share is computed on the device
+// right after the encode kernel and only the digests come back.
+static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                              const uint8_t *data, size_t chunk_len, uint32_t nchunks,
+                              uint8_t *parity_out, uint8_t *hashes_out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (chunk_len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
+  const uint32_t p = n - k;
+  if (nchunks == 0) return STORB_RS_OK;
+  if (p > 0 && !parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  const size_t B = (chunk_len + k - 1) / k;
+  if (hashes_out && B > 16ull * 1024 * 1024)
+    return fail(ctx, STORB_RS_EINVAL, "blake3: share larger than 16 MiB");
+  const size_t S = round_up(B, kAlign);
+  const bool packed = (S == B) && (B * k == chunk_len);
+  // ~64 MiB of input per batch keeps both DMA directions busy.
+  const size_t per = static_cast<size_t>(k) * S;
+  uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
+  batch = std::min(batch, nchunks);
+  const size_t hash_bytes = hashes_out ? static_cast<size_t>(batch) * n * 32 : 0;
+  // Caller buffers that are page-locked (storb_rs_host_alloc / _register)
+  // are DMA'd directly: no pack copy in, no unpack copy out.
+  const bool in_direct = packed && range_pinned(data, static_cast<size_t>(nchunks) * chunk_len);
+  const bool out_direct =
+      p > 0 && S == B && range_pinned(parity_out, static_cast<size_t>(nchunks) * p * B);
+  // Page-locked caller chunks without piece ids: the kernel reads them (and
+  // writes parity) over PCIe directly (zero-copy). Kernel-driven PCIe
+  // traffic overlaps both directions, where the SDMA copies of H2D and D2H
+  // share one ceiling (57 GB/s total, tools/pcie_probe.py): 47 vs 35 GiB/s
+  // measured. From pageable chunks the SDMA pipeline stays ahead (34 vs
+  // 20 GiB/s: the host's packing competes with the kernel's reads of the
+  // same staging), and the hashed path keeps the shares on the device.
+  const bool zc = ctx->zc_batch && !hashes_out && p > 0 && in_direct;
+  DeviceGuard g(ctx->device);
+  for (int b = 0; b < 2; b++) {
+    if (!in_direct) HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
+    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch + hash_bytes));
+    if (!zc)
+      HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
+  }
+  const uint32_t nb = (nchunks + batch - 1) / batch;
+  HostPool &pool = host_pool(ctx);
+  auto unpack = [&](uint32_t bi) {
+    const int b = bi & 1;
+    const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
+    if (p > 0 && !out_direct) {
+      if (S == B) {
+        pool.copy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
+                  static_cast<size_t>(cn) * p * B);
+      } else {
+        pool.run(static_cast<int>(cn), [&](int c) {
+          for (uint32_t i = 0; i < p; i++)
+            std::memcpy(parity_out + ((static_cast<size_t>(c0) + c) * p + i) * B,
+                        ctx->pipe_out[b].p + (static_cast<size_t>(c) * p + i) * S, B);
+        });
+      }
+    }
+    if (hashes_out) {
+      // device order: [c][j] data digests, then [c][i] parity digests
+      const uint8_t *hd = ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch;
+      const uint8_t *hp = hd + static_cast<size_t>(cn) * k * 32;
+      for (uint32_t c = 0; c < cn; c++) {
+        uint8_t *o = hashes_out + (static_cast<size_t>(c0) + c) * n * 32;
+        std::memcpy(o, hd + static_cast<size_t>(c) * k * 32, static_cast<size_t>(k) * 32);
+        std::memcpy(o + static_cast<size_t>(k) * 32, hp + static_cast<size_t>(c) * p * 32,
+                    static_cast<size_t>(p) * 32);
+      }
+    }
+  };
+  for (uint32_t bi = 0; bi < nb; bi++) {
+    const int b = bi & 1;
+    hipStream_t s = ctx->pipe[b];
+    // Pinned buffer pair b is free once batch bi-2 has landed (device
+    // buffers are reused in stream order and need no host wait).
+    if (bi >= 2 && !(in_direct && (out_direct || p == 0) && !hashes_out)) {
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      unpack(bi - 2);
+    }
+    const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
+    const uint8_t *hin = in_direct ? data + static_cast<size_t>(c0) * chunk_len
+                                   : ctx->pipe_in[b].p;
+    if (in_direct) {
+      // the H2D below reads the caller's page-locked chunks in place
+    } else if (packed) {
+      pool.copy(ctx->pipe_in[b].p, data + static_cast<size_t>(c0) * chunk_len, per * cn);
+    } else {
+      pool.run(static_cast<int>(cn), [&](int c) {
+        const uint8_t *src = data + (static_cast<size_t>(c0) + c) * chunk_len;
+        for (uint32_t j = 0; j < k; j++) {
+          const size_t off = static_cast<size_t>(j) * B;
+          const size_t cnt = off < chunk_len ? std::min(B, chunk_len - off) : 0;
+          uint8_t *dst = ctx->pipe_in[b].p + static_cast<size_t>(c) * per +
+                         static_cast<size_t>(j) * S;
+          if (cnt) std::memcpy(dst, src + off, cnt);
+          std::memset(dst + cnt, 0, S - cnt);
+        }
+      });
+    }
+    if (zc) {  // the kernel reads the pinned chunks and writes pinned parity over PCIe
+      uint8_t *di, *dq;
+      HIP_TRY(ctx, host_dev_ptr(const_cast<uint8_t *>(hin), &di));
+      HIP_TRY(ctx, host_dev_ptr(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
+                                           : ctx->pipe_out[b].p,
+                                &dq));
+      std::vector<const uint8_t *> in(k);
+      std::vector<uint8_t *> out(p);
+      std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
+      for (uint32_t j = 0; j < k; j++) in[j] = di + static_cast<size_t>(j) * S;
+      for (uint32_t i = 0; i < p; i++) out[i] = dq + static_cast<size_t>(i) * S;
+      const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S,
+                                  cn, s);
+      if (rc) return rc;
+      continue;
+    }
+    uint8_t *dd = ctx->pipe_dev[b].p;
+    uint8_t *dp = dd + per * batch;
+    uint8_t *dh = dp + static_cast<size_t>(p) * S * batch;  // digests (if any)
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
+    if (p > 0) {
+      std::vector<const uint8_t *> in(k);
+      std::vector<uint8_t *> out(p);
+      std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
+      for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
+      for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
+      const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S,
+                                  cn, s);
+      if (rc) return rc;
+    }
+    size_t back = static_cast<size_t>(p) * S * cn;
+    if (hashes_out) {
+      // shares are pitched S apart across the whole batch: one launch each
+      HIP_TRY(ctx, launch_blake3_batch(dd, B, cn * k, S, dh, s));
+      if (p > 0)
+        HIP_TRY(ctx, launch_blake3_batch(dp, B, cn * p, S, dh + static_cast<size_t>(cn) * k * 32,
+                                         s));
+    }
+    if (back)
+      HIP_TRY(ctx, hipMemcpyAsync(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
+                                             : ctx->pipe_out[b].p,
+                                  dp, back, hipMemcpyDeviceToHost, s));
+    if (hashes_out)
+      HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch, dh,
+                                  static_cast<size_t>(cn) * n * 32, hipMemcpyDeviceToHost, s));
+  }
+  for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[bi & 1]));
+    unpack(bi);
+  }
+  return STORB_RS_OK;
+}
+
+// Pipelined batch decode (the download path, download.rs:453-465, one
+// chunk after another today). Every chunk selects its first k shares by
+// index (decode_chunk, piece.rs:368-381). Chunks whose k data shares are all
+// present are pure host copies; the rest are grouped by erasure pattern, so
+// each batch is one launch of one decode matrix, and stream through the same
+// double-buffered pinned pipeline as encode: pack the k survivors into
+// pinned staging (present data shares also go straight to `out`), H2D,
+// rebuild only the missing rows, D2H them, unpack into `out`.
+int storb_rs_decode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                           size_t padlen, uint32_t nchunks, const uint8_t *const *shares,
+                           const uint32_t *share_idx, const uint32_t *nshares, uint8_t *out,
+                           size_t out_stride) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (nchunks == 0) return STORB_RS_OK;
+  if (!shares || !share_idx || !nshares || !out || block == 0 ||
+      padlen >= static_cast<size_t>(k) * block)
+    return fail(ctx, STORB_RS_EINVAL, "decode_chunks: bad arguments");
+  const size_t outlen = static_cast<size_t>(k) * block - padlen;
+  if (out_stride == 0) out_stride = outlen;
+  if (out_stride < outlen) return fail(ctx, STORB_RS_EINVAL, "decode_chunks: out_stride < chunk");
+  // per chunk: its k slot shares (pointers) and erasure pattern
+  std::vector<const uint8_t *> slot_ptr(static_cast<size_t>(nchunks) * k);
+  std::map<std::vector<uint32_t>, std::vector<uint32_t>> groups;
+  std::vector<uint32_t> plain;
+  size_t off = 0;
+  for (uint32_t c = 0; c < nchunks; c++) {
+    std::vector<uint32_t> slot_idx, slot_pos;
+    const int rc = select_shares(ctx, k, n, share_idx + off, nshares[c], slot_idx, slot_pos);
+    if (rc) {
+      ctx->last_error += " (chunk " + std::to_string(c) + ")";
+      return rc;
+    }
+    for (uint32_t s = 0; s < k; s++) {
+      slot_ptr[static_cast<size_t>(c) * k + s] = shares[off + slot_pos[s]];
+      if (!slot_ptr[static_cast<size_t>(c) * k + s])
+        return fail(ctx, STORB_RS_EINVAL, "decode_chunks: null share");
+    }
+    off += nshares[c];
+    bool all_data = true;
+    for (uint32_t s = 0; s < k; s++) all_data &= slot_idx[s] == s;
+    if (all_data)
+      plain.push_back(c);
+    else
+      groups[slot_idx].push_back(c);
+  }
+  HostPool &pool = host_pool(ctx);
+  auto put_row = [&](uint32_t c, uint32_t row, const uint8_t *src) {
+    const size_t o = static_cast<size_t>(row) * block;
+    if (o < outlen)
+      std::memcpy(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
+  };
+  if (!plain.empty())  // all data shares present: concatenation (zfec does the same)
+    pool.run(static_cast<int>(plain.size()), [&](int i) {
+      for (uint32_t s = 0; s < k; s++)
+        put_row(plain[i], s, slot_ptr[static_cast<size_t>(plain[i]) * k + s]);
+    });
+  if (groups.empty()) return STORB_RS_OK;
+
+  struct Item {
+    const std::vector<uint32_t> *slots;
+    const uint32_t *chunks;
+    uint32_t cn;
+    std::vector<uint8_t> coef;
+    std::vector<uint32_t> missing;
+  };
+  const size_t S = round_up(block, kAlign);
+  const size_t per = static_cast<size_t>(k) * S;
+  uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
+  std::vector<Item> items;
+  uint32_t emax = 0;
+  for (auto &g : groups) {
+    std::vector<uint8_t> coef;
+    std::vector<uint32_t> missing;
+    const int rc = decode_rows(ctx, k, n, g.first, coef, missing);
+    if (rc) return rc;
+    emax = std::max<uint32_t>(emax, static_cast<uint32_t>(missing.size()));
+    for (size_t i = 0; i < g.second.size(); i += batch)
+      items.push_back(Item{&g.first, g.second.data() + i,
+                           static_cast<uint32_t>(std::min<size_t>(batch, g.second.size() - i)),
+                           coef, missing});
+  }
+  batch = 0;
+  for (auto &it : items) batch = std::max(batch, it.cn);
+  DeviceGuard dg(ctx->device);
+  for (int b = 0; b < 2; b++) {
+    HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
+    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(emax) * S * batch));
+    HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(k + emax) * S * batch));
+  }
+  auto unpack = [&](size_t ii) {
+    const Item &it = items[ii];
+    const uint8_t *src = ctx->pipe_out[ii & 1].p;
+    const uint32_t e = static_cast<uint32_t>(it.missing.size());
+    pool.run(static_cast<int>(it.cn), [&](int c) {
+      for (uint32_t r = 0; r < e; r++)
+        put_row(it.chunks[c], it.missing[r], src + (static_cast<size_t>(c) * e + r) * S);
+    });
+  };
+  for (size_t ii = 0; ii < items.size(); ii++) {
+    const int b = ii & 1;
+    hipStream_t s = ctx->pipe[b];
+    if (ii >= 2) {  // pinned pair b is free once item ii-2 has landed
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      unpack(ii - 2);
+    }
+    const Item &it = items[ii];
+    const uint32_t e = static_cast<uint32_t>(it.missing.size());
+    uint8_t *hin = ctx->pipe_in[b].p;
+    pool.run(static_cast<int>(it.cn), [&](int c) {
+      const uint32_t ch = it.chunks[c];
+      for (uint32_t sl = 0; sl < k; sl++) {
+        const uint8_t *src = slot_ptr[static_cast<size_t>(ch) * k + sl];
+        uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(sl) * S;
+        std::memcpy(dst, src, block);
+        if (S > block) std::memset(dst + block, 0, S - block);
+        if ((*it.slots)[sl] == sl) put_row(ch, sl, src);  // present data share
+      }
+    });
+    uint8_t *dd = ctx->pipe_dev[b].p;
+    uint8_t *dm = dd + per * it.cn;
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * it.cn, hipMemcpyHostToDevice, s));
+    std::vector<const uint8_t *> in(k);
+    std::vector<uint8_t *> o(e);
+    std::vector<size_t> ins(k, per), outs(e, static_cast<size_t>(e) * S);
+    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
+    for (uint32_t r = 0; r < e; r++) o[r] = dm + static_cast<size_t>(r) * S;
+    const int rc = apply(ctx, k, e, it.coef.data(), in.data(), ins.data(), o.data(), outs.data(),
+                         S, it.cn, s);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(e) * S * it.cn,
+                                hipMemcpyDeviceToHost, s));
+  }
+  for (size_t ii = items.size() >= 2 ? items.size() - 2 : 0; ii < items.size(); ii++) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[ii & 1]));
+    unpack(ii);
+  }
+  return STORB_RS_OK;
+}
+
+int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                           size_t chunk_len, uint32_t nchunks, uint8_t *parity_out) {
+  return encode_chunks_impl(ctx, k, n, data, chunk_len, nchunks, parity_out, nullptr);
+}
+
+int storb_rs_encode_chunks_hashed(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                                  const uint8_t *data, size_t chunk_len, uint32_t nchunks,
+                                  uint8_t *parity_out, uint8_t *hashes_out) {
+  if (!hashes_out) return STORB_RS_EINVAL;
+  return encode_chunks_impl(ctx, k, n, data, chunk_len, nchunks, parity_out, hashes_out);
+}
+
+}  // extern "C"

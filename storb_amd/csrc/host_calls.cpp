@@ -1,0 +1,339 @@
+// host_calls.cpp -- single-chunk host calls of the C ABI: the entry points
+// the zfec-rs shim reaches once per chunk (Fec::encode, piece.rs:329;
+// Fec::decode, piece.rs:384-386) and host-side repair. Each call runs the
+// kernel on page-locked staging mapped into the GPU (zero-copy over PCIe),
+// uses page-locked caller buffers in place, and overlaps the staging copies
+// of pageable ones with the kernel over column slices.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "ctx.hpp"
+
+using namespace storb_rs;
+using namespace storb_rs::detail;
+
+namespace storb_rs {
+namespace detail {
+
+// Single-call pipeline over column slices of one stripe. A chunk's shares
+// are split into q column ranges [off, off+cnt) (16-B multiples); while the
+// kernel works on slice t (zero-copy, over PCIe), the host packs slice t+1
+// into pinned staging and unpacks slice t-1's outputs, so the staging copies
+// of pageable caller buffers overlap the kernel instead of adding to it.
+// q = 1 (small chunks) degenerates to pack -> launch -> sync -> unpack.
+int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)> &pack,
+           const std::function<int(size_t, size_t)> &launch,
+           const std::function<void(size_t, size_t)> &unpack) {
+  int q = static_cast<int>(std::min<size_t>(kMaxSlices, S / (128u << 10)));
+  if (q < 2) q = 1;
+  const size_t slice = round_up((S + q - 1) / q, kAlign);
+  q = static_cast<int>((S + slice - 1) / slice);
+  for (int t = 0; t < q; t++)
+    if (!ctx->slice_ev[t])
+      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->slice_ev[t], hipEventDisableTiming));
+  auto range = [&](int t, size_t &off, size_t &cnt) {
+    off = static_cast<size_t>(t) * slice;
+    cnt = std::min(slice, S - off);
+  };
+  for (int t = 0; t < q; t++) {
+    size_t off, cnt;
+    range(t, off, cnt);
+    pack(off, cnt);
+    const int rc = launch(off, cnt);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->slice_ev[t], ctx->stream));
+    if (t > 0) {
+      HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[t - 1]));
+      range(t - 1, off, cnt);
+      unpack(off, cnt);
+    }
+  }
+  size_t off, cnt;
+  range(q - 1, off, cnt);
+  HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[q - 1]));
+  unpack(off, cnt);
+  return STORB_RS_OK;
+}
+
+}  // namespace detail
+}  // namespace storb_rs
+
+extern "C" {
+
+int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                    size_t len, uint8_t *const *parity_out, size_t *block_out,
+                    size_t *padlen_out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
+  const size_t B = (len + k - 1) / k, pad = B * k - len;
+  if (block_out) *block_out = B;
+  if (padlen_out) *padlen_out = pad;
+  const uint32_t p = n - k;
+  if (p == 0) return STORB_RS_OK;
+  if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  for (uint32_t i = 0; i < p; i++)
+    if (!parity_out[i]) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  const size_t S = round_up(B, kAlign);
+  const bool zc = static_cast<size_t>(n) * S <= ctx->zc_max;
+  // Page-locked, 16-B aligned caller buffers need no staging at all.
+  auto aligned = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool in_direct = zc && pad == 0 && S == B && aligned(data) && range_pinned(data, len);
+  bool out_direct = zc && S == B;
+  for (uint32_t i = 0; out_direct && i < p; i++)
+    out_direct = aligned(parity_out[i]) && range_pinned(parity_out[i], B);
+  DeviceGuard g(ctx->device);
+  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(p) * S));
+  if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(n) * S));
+  HostPool &pool = host_pool(ctx);
+  hipStream_t s = ctx->stream;
+  std::vector<const uint8_t *> in(k);
+  std::vector<uint8_t *> out(p);
+  std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(p, static_cast<size_t>(p) * S);
+  // Zero-padded data shares, S-pitched (zfec pads the tail with zeros):
+  // columns [off, off + cnt) of every share into pinned staging.
+  auto pack = [&](size_t off, size_t cnt) {
+    const int parts = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
+    pool.run(parts, [&](int part) {
+      for (uint32_t j = static_cast<uint32_t>(part); j < k; j += parts) {
+        const size_t src = static_cast<size_t>(j) * B + off;
+        size_t avail = off < B ? std::min(cnt, B - off) : 0;
+        avail = src < len ? std::min(avail, len - src) : 0;
+        uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(j) * S + off;
+        if (avail) std::memcpy(dst, data + src, avail);
+        if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
+      }
+    });
+  };
+  auto unpack = [&](size_t off, size_t cnt) {
+    const size_t c = off < B ? std::min(cnt, B - off) : 0;
+    if (!c) return;
+    const int parts = static_cast<size_t>(p) * c >= (2u << 20) ? static_cast<int>(p) : 1;
+    pool.run(parts, [&](int part) {
+      for (uint32_t i = static_cast<uint32_t>(part); i < p; i += parts)
+        std::memcpy(parity_out[i] + off, ctx->pin_out.p + static_cast<size_t>(i) * S + off, c);
+    });
+  };
+  if (zc) {  // the kernel reads and writes page-locked host memory over PCIe
+    uint8_t *dd, *dp = nullptr;
+    HIP_TRY(ctx, host_dev_ptr(in_direct ? const_cast<uint8_t *>(data) : ctx->pin_in.p, &dd));
+    std::vector<uint8_t *> pd(p);
+    if (out_direct) {
+      for (uint32_t i = 0; i < p; i++) HIP_TRY(ctx, host_dev_ptr(parity_out[i], &pd[i]));
+    } else {
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dp));
+      for (uint32_t i = 0; i < p; i++) pd[i] = dp + static_cast<size_t>(i) * S;
+    }
+    auto launch = [&](size_t off, size_t cnt) {
+      for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S + off;
+      for (uint32_t i = 0; i < p; i++) out[i] = pd[i] + off;
+      return encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), cnt, 1, s);
+    };
+    if (in_direct && out_direct) {  // nothing to overlap
+      const int rc = launch(0, S);
+      if (rc) return rc;
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      return STORB_RS_OK;
+    }
+    return sliced(
+        ctx, S, [&](size_t off, size_t cnt) { if (!in_direct) pack(off, cnt); }, launch,
+        [&](size_t off, size_t cnt) { if (!out_direct) unpack(off, cnt); });
+  }
+  pack(0, S);
+  uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
+  HIP_TRY(ctx, hipMemcpyAsync(dd, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                              hipMemcpyHostToDevice, s));
+  for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
+  for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
+  int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S, 1, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dp, static_cast<size_t>(p) * S,
+                              hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  unpack(0, S);
+  return STORB_RS_OK;
+}
+
+int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+                    const uint32_t *share_idx, uint32_t nshares, size_t block,
+                    size_t padlen, uint8_t *out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (!shares || !share_idx || !out || block == 0 ||
+      padlen >= static_cast<size_t>(k) * block)
+    return fail(ctx, STORB_RS_EINVAL, "decode: bad arguments");
+  std::vector<uint32_t> slot_idx, slot_pos, missing;
+  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint8_t> coef;
+  rc = decode_rows(ctx, k, n, slot_idx, coef, missing);
+  if (rc) return rc;
+  const size_t outlen = static_cast<size_t>(k) * block - padlen;
+  auto put = [&](uint32_t row, const uint8_t *src) {
+    const size_t off = static_cast<size_t>(row) * block;
+    if (off < outlen) std::memcpy(out + off, src, std::min(block, outlen - off));
+  };
+  HostPool &pool = host_pool(ctx);
+  const int parts = static_cast<size_t>(k) * block >= (1u << 20) ? static_cast<int>(k) : 1;
+  auto put_present = [&] {  // surviving data shares: plain copies into out
+    pool.run(parts, [&](int part) {
+      for (uint32_t s = static_cast<uint32_t>(part); s < k; s += parts)
+        if (slot_idx[s] < k) put(s, shares[slot_pos[s]]);
+    });
+  };
+  if (missing.empty()) {  // all data shares present: concatenation, as zfec
+    put_present();
+    return STORB_RS_OK;
+  }
+  const size_t S = round_up(block, kAlign);
+  const uint32_t e = static_cast<uint32_t>(missing.size());
+  const bool zc = static_cast<size_t>(k + e) * S <= ctx->zc_max;
+  auto aligned = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  // Page-locked, aligned caller shares / output are used in place.
+  bool in_direct = zc && S == block;
+  for (uint32_t c = 0; in_direct && c < k; c++)
+    in_direct = aligned(shares[slot_pos[c]]) && range_pinned(shares[slot_pos[c]], block);
+  const bool out_direct = zc && S == block && padlen == 0 && aligned(out) &&
+                          range_pinned(out, outlen);
+  DeviceGuard g(ctx->device);
+  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(e) * S));
+  if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + e) * S));
+  // columns [off, off + cnt) of row `row` of the chunk (truncated at outlen)
+  auto put_cols = [&](uint32_t row, size_t off, size_t cnt, const uint8_t *src) {
+    const size_t o = static_cast<size_t>(row) * block + off;
+    size_t c = off < block ? std::min(cnt, block - off) : 0;
+    c = o < outlen ? std::min(c, outlen - o) : 0;
+    if (c) std::memcpy(out + o, src, c);
+  };
+  // slot shares into pinned staging; present data shares also into out
+  auto pack = [&](size_t off, size_t cnt) {
+    const int pp = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
+    pool.run(pp, [&](int part) {
+      for (uint32_t c = static_cast<uint32_t>(part); c < k; c += pp) {
+        const uint8_t *src = shares[slot_pos[c]] + off;
+        const size_t avail = off < block ? std::min(cnt, block - off) : 0;
+        if (!in_direct) {
+          uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(c) * S + off;
+          if (avail) std::memcpy(dst, src, avail);
+          if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
+        }
+        if (slot_idx[c] < k) put_cols(c, off, cnt, src);
+      }
+    });
+  };
+  auto unpack = [&](size_t off, size_t cnt) {
+    if (out_direct) return;
+    for (uint32_t r = 0; r < e; r++)
+      put_cols(missing[r], off, cnt, ctx->pin_out.p + static_cast<size_t>(r) * S + off);
+  };
+  hipStream_t s = ctx->stream;
+  std::vector<const uint8_t *> in(k);
+  std::vector<uint8_t *> o(e);
+  std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(e, static_cast<size_t>(e) * S);
+  if (zc) {  // zero-copy: the kernel reads / writes page-locked host memory
+    std::vector<uint8_t *> id(k), od(e);
+    uint8_t *base = nullptr;
+    if (in_direct) {
+      for (uint32_t c = 0; c < k; c++)
+        HIP_TRY(ctx, host_dev_ptr(const_cast<uint8_t *>(shares[slot_pos[c]]), &id[c]));
+    } else {
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &base));
+      for (uint32_t c = 0; c < k; c++) id[c] = base + static_cast<size_t>(c) * S;
+    }
+    if (out_direct) {
+      HIP_TRY(ctx, host_dev_ptr(out, &base));
+      for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(missing[r]) * block;
+    } else {
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &base));
+      for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(r) * S;
+    }
+    auto launch = [&](size_t off, size_t cnt) {
+      for (uint32_t c = 0; c < k; c++) in[c] = id[c] + off;
+      for (uint32_t r = 0; r < e; r++) o[r] = od[r] + off;
+      return apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), cnt, 1,
+                   s);
+    };
+    if (in_direct && out_direct) {
+      rc = launch(0, S);
+      if (rc) return rc;
+      put_present();  // host copies overlap the kernel (disjoint rows of out)
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      return STORB_RS_OK;
+    }
+    return sliced(ctx, S, pack, launch, unpack);
+  }
+  pack(0, S);
+  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
+  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                              hipMemcpyHostToDevice, s));
+  for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
+  for (uint32_t r = 0; r < e; r++) o[r] = dout + static_cast<size_t>(r) * S;
+  rc = apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1, s);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(e) * S,
+                              hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  unpack(0, S);
+  return STORB_RS_OK;
+}
+
+int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+                    const uint32_t *share_idx, uint32_t nshares, size_t block,
+                    const uint32_t *targets, uint32_t ntargets, uint8_t *const *out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (!shares || !share_idx || (ntargets && (!targets || !out)) || block == 0)
+    return fail(ctx, STORB_RS_EINVAL, "repair: bad arguments");
+  std::vector<uint32_t> slot_idx, slot_pos;
+  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint8_t> coef;
+  rc = repair_rows(ctx, k, n, slot_idx, targets, ntargets, coef);
+  if (rc || ntargets == 0) return rc;
+  const size_t S = round_up(block, kAlign);
+  DeviceGuard g(ctx->device);
+  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
+  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(ntargets) * S));
+  HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + ntargets) * S));
+  for (uint32_t c = 0; c < k; c++) {
+    std::memcpy(ctx->pin_in.p + static_cast<size_t>(c) * S, shares[slot_pos[c]], block);
+    std::memset(ctx->pin_in.p + static_cast<size_t>(c) * S + block, 0, S - block);
+  }
+  hipStream_t s = ctx->stream;
+  const bool zc = static_cast<size_t>(k + ntargets) * S <= ctx->zc_max;
+  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
+  if (zc) {  // zero-copy: the kernel works on the pinned staging directly
+    HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &din));
+    HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dout));
+  } else {
+    HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+                                hipMemcpyHostToDevice, s));
+  }
+  std::vector<const uint8_t *> in(k);
+  std::vector<uint8_t *> o(ntargets);
+  std::vector<size_t> ins(k, static_cast<size_t>(k) * S),
+      outs(ntargets, static_cast<size_t>(ntargets) * S);
+  for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
+  for (uint32_t r = 0; r < ntargets; r++) o[r] = dout + static_cast<size_t>(r) * S;
+  rc = apply(ctx, k, ntargets, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1,
+             s);
+  if (rc) return rc;
+  if (!zc)
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(ntargets) * S,
+                                hipMemcpyDeviceToHost, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  for (uint32_t r = 0; r < ntargets; r++)
+    std::memcpy(out[r], ctx->pin_out.p + static_cast<size_t>(r) * S, block);
+  return STORB_RS_OK;
+}
+
+}  // extern "C"

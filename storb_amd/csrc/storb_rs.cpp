@@ -1,10 +1,12 @@
-// storb_rs.cpp -- implementation of the C ABI in include/storb_rs.h.
+// storb_rs.cpp -- implementation of the C ABI in include/storb_rs.h (with
+// host_calls.cpp and host_batch.cpp; shared internals in ctx.hpp).
 //
 // Host side of the MI355X Reed-Solomon path: parameter checks and generator
 // matrices (mirroring zfec-rs Fec::new, reached from piece.rs:328,383),
 // decode-matrix construction (Fec::decode, piece.rs:384-386), coefficient
-// table caches, pinned staging, streams, and the tiling of arbitrary
-// (rows x k) matrices onto the 16 x 32 slot kernels of rs_kernels.hip.
+// table caches, streams, the tiling of arbitrary (rows x k) matrices onto the
+// 16 x 32 slot kernels of rs_kernels.hip, the device-resident batched calls,
+// blake3 piece ids and the page-locked host registry.
 #include "../../include/storb_rs.h"
 
 #include <hip/hip_runtime_api.h>
@@ -24,78 +26,16 @@
 #include <vector>
 
 #include "blake3.hpp"
-#include "gf256.hpp"
-#include "host_pool.hpp"
-#include "rs_kernels.hpp"
+#include "ctx.hpp"
 
 using namespace storb_rs;
+using namespace storb_rs::detail;
 
-namespace {
+namespace storb_rs {
+namespace detail {
 
-constexpr size_t kAlign = 16;
-constexpr int kMaxSlices = 8;
-inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
-
-struct DevBuf {
-  uint8_t *p = nullptr;
-  size_t cap = 0;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-  hipError_t ensure(size_t n) {
-    if (n <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), n);
-    if (e == hipSuccess) cap = n;
-    return e;
-  }
-};
-
-struct PinBuf {
-  uint8_t *p = nullptr;
-  size_t cap = 0;
-  ~PinBuf() {
-    if (p) (void)hipHostFree(p);
-  }
-  hipError_t ensure(size_t n) {
-    if (n <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault);
-    if (e == hipSuccess) cap = n;
-    return e;
-  }
-};
-
-// Device-resident coefficient tables for one (rows x k) matrix, tiled in
-// kSlotR x kSlotK blocks: for block b, ptab + b_off[b] PermTabs and
-// btab + b_off[b]*256 product-table bytes.
-struct Tables {
-  uint8_t *dev = nullptr;
-  size_t perm_bytes = 0;
-  std::vector<size_t> b_off;
-  ~Tables() {
-    if (dev) (void)hipFree(dev);
-  }
-};
-
-struct DeviceGuard {
-  int prev = -1;
-  bool ok = false;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    ok = hipSetDevice(dev) == hipSuccess;
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
-
-std::mutex g_enc_mu;
-std::map<std::pair<uint32_t, uint32_t>, std::vector<uint8_t>> g_enc;
+static std::mutex g_enc_mu;
+static std::map<std::pair<uint32_t, uint32_t>, std::vector<uint8_t>> g_enc;
 
 const std::vector<uint8_t> &cached_enc(uint32_t k, uint32_t n) {
   std::lock_guard<std::mutex> lk(g_enc_mu);
@@ -105,13 +45,15 @@ const std::vector<uint8_t> &cached_enc(uint32_t k, uint32_t n) {
   return it->second;
 }
 
-std::atomic<int> g_rr{0};
+static std::atomic<int> g_rr{0};
+
+int next_round_robin() { return g_rr.fetch_add(1); }
 
 // Page-locked host ranges the caller obtained through storb_rs_host_alloc or
 // storb_rs_host_register. The pipelined host path DMAs straight from / into
 // such ranges instead of staging through its own pinned buffers.
-std::mutex g_pin_mu;
-std::map<uintptr_t, std::pair<size_t, bool>> g_pinned;  // base -> (len, allocated here)
+static std::mutex g_pin_mu;
+static std::map<uintptr_t, std::pair<size_t, bool>> g_pinned;  // base -> (len, allocated here)
 
 bool range_pinned(const void *p, size_t len) {
   if (!p || len == 0) return false;
@@ -123,49 +65,6 @@ bool range_pinned(const void *p, size_t len) {
   return a - it->first + len <= it->second.first;
 }
 
-}  // namespace
-
-struct storb_rs_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipStream_t pipe[2] = {nullptr, nullptr};
-  int variant = STORB_RS_KERNEL_AUTO;
-  std::mutex mu;
-  std::string last_error;
-  DevBuf stage;
-  DevBuf pipe_dev[2];
-  PinBuf pin_in, pin_out;
-  PinBuf pipe_in[2], pipe_out[2];
-  std::map<std::vector<uint8_t>, std::unique_ptr<Tables>> tables;
-  std::unique_ptr<HostPool> pool;  // host copy workers, created on first use
-  // Single-call paths whose staged bytes (in + out) are at most this size
-  // run the kernel straight on the pinned staging buffers (zero-copy over
-  // PCIe) instead of DMA in -> kernel -> DMA out: one launch and one sync
-  // instead of three operations. STORB_RS_ZC_MAX, bytes; 0 disables.
-  size_t zc_max = 0;
-  // storb_rs_encode_chunks without piece ids: zero-copy kernels (1) or
-  // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
-  bool zc_batch = true;
-  hipEvent_t slice_ev[kMaxSlices] = {};  // sliced single-call pipeline
-};
-
-namespace {
-
-int fail(storb_rs_ctx *ctx, int code, const std::string &msg) {
-  if (ctx) ctx->last_error = msg;
-  return code;
-}
-
-int hip_fail(storb_rs_ctx *ctx, hipError_t e, const char *what) {
-  std::string m = std::string(what) + ": " + hipGetErrorString(e);
-  return fail(ctx, e == hipErrorOutOfMemory ? STORB_RS_ENOMEM : STORB_RS_EDEVICE, m);
-}
-
-#define HIP_TRY(ctx, expr)                              \
-  do {                                                  \
-    hipError_t e_ = (expr);                             \
-    if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
-  } while (0)
 
 Variant pick_variant(const storb_rs_ctx *ctx) {
   return ctx->variant == STORB_RS_KERNEL_LDS ? Variant::Lds : Variant::Perm;
@@ -414,47 +313,10 @@ hipError_t host_dev_ptr(uint8_t *host, uint8_t **dev) {
   return e;
 }
 
-// Single-call pipeline over column slices of one stripe. A chunk's shares
-// are split into q column ranges [off, off+cnt) (16-B multiples); while the
-// kernel works on slice t (zero-copy, over PCIe), the host packs slice t+1
-// into pinned staging and unpacks slice t-1's outputs, so the staging copies
-// of pageable caller buffers overlap the kernel instead of adding to it.
-// q = 1 (small chunks) degenerates to pack -> launch -> sync -> unpack.
-int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)> &pack,
-           const std::function<int(size_t, size_t)> &launch,
-           const std::function<void(size_t, size_t)> &unpack) {
-  int q = static_cast<int>(std::min<size_t>(kMaxSlices, S / (128u << 10)));
-  if (q < 2) q = 1;
-  const size_t slice = round_up((S + q - 1) / q, kAlign);
-  q = static_cast<int>((S + slice - 1) / slice);
-  for (int t = 0; t < q; t++)
-    if (!ctx->slice_ev[t])
-      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->slice_ev[t], hipEventDisableTiming));
-  auto range = [&](int t, size_t &off, size_t &cnt) {
-    off = static_cast<size_t>(t) * slice;
-    cnt = std::min(slice, S - off);
-  };
-  for (int t = 0; t < q; t++) {
-    size_t off, cnt;
-    range(t, off, cnt);
-    pack(off, cnt);
-    const int rc = launch(off, cnt);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipEventRecord(ctx->slice_ev[t], ctx->stream));
-    if (t > 0) {
-      HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[t - 1]));
-      range(t - 1, off, cnt);
-      unpack(off, cnt);
-    }
-  }
-  size_t off, cnt;
-  range(q - 1, off, cnt);
-  HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[q - 1]));
-  unpack(off, cnt);
-  return STORB_RS_OK;
-}
+}  // namespace detail
+}  // namespace storb_rs
 
-}  // namespace
+
 
 // ======================================================================
 extern "C" {
@@ -485,7 +347,7 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   const int ndev = storb_rs_device_count();
   if (ndev <= 0) return STORB_RS_ENODEV;
   int dev = device_ordinal;
-  if (dev < 0) dev = g_rr.fetch_add(1) % ndev;
+  if (dev < 0) dev = next_round_robin() % ndev;
   if (dev >= ndev) return STORB_RS_EINVAL;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return STORB_RS_ENODEV;
@@ -825,588 +687,6 @@ int storb_rs_fill_splitmix_dev(storb_rs_ctx *ctx, uint8_t *d, size_t obj_len,
   HIP_TRY(ctx, launch_fill_splitmix(d, obj_len, nobj, obj_stride, seed_base,
                                     pick_stream(ctx, hip_stream)));
   return STORB_RS_OK;
-}
-
-// ------------------------------------------------------------------ host
-int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
-                    size_t len, uint8_t *const *parity_out, size_t *block_out,
-                    size_t *padlen_out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
-  if (len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
-  const size_t B = (len + k - 1) / k, pad = B * k - len;
-  if (block_out) *block_out = B;
-  if (padlen_out) *padlen_out = pad;
-  const uint32_t p = n - k;
-  if (p == 0) return STORB_RS_OK;
-  if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
-  for (uint32_t i = 0; i < p; i++)
-    if (!parity_out[i]) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
-  const size_t S = round_up(B, kAlign);
-  const bool zc = static_cast<size_t>(n) * S <= ctx->zc_max;
-  // Page-locked, 16-B aligned caller buffers need no staging at all.
-  auto aligned = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  const bool in_direct = zc && pad == 0 && S == B && aligned(data) && range_pinned(data, len);
-  bool out_direct = zc && S == B;
-  for (uint32_t i = 0; out_direct && i < p; i++)
-    out_direct = aligned(parity_out[i]) && range_pinned(parity_out[i], B);
-  DeviceGuard g(ctx->device);
-  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(p) * S));
-  if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(n) * S));
-  HostPool &pool = host_pool(ctx);
-  hipStream_t s = ctx->stream;
-  std::vector<const uint8_t *> in(k);
-  std::vector<uint8_t *> out(p);
-  std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(p, static_cast<size_t>(p) * S);
-  // Zero-padded data shares, S-pitched (zfec pads the tail with zeros):
-  // columns [off, off + cnt) of every share into pinned staging.
-  auto pack = [&](size_t off, size_t cnt) {
-    const int parts = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
-    pool.run(parts, [&](int part) {
-      for (uint32_t j = static_cast<uint32_t>(part); j < k; j += parts) {
-        const size_t src = static_cast<size_t>(j) * B + off;
-        size_t avail = off < B ? std::min(cnt, B - off) : 0;
-        avail = src < len ? std::min(avail, len - src) : 0;
-        uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(j) * S + off;
-        if (avail) std::memcpy(dst, data + src, avail);
-        if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
-      }
-    });
-  };
-  auto unpack = [&](size_t off, size_t cnt) {
-    const size_t c = off < B ? std::min(cnt, B - off) : 0;
-    if (!c) return;
-    const int parts = static_cast<size_t>(p) * c >= (2u << 20) ? static_cast<int>(p) : 1;
-    pool.run(parts, [&](int part) {
-      for (uint32_t i = static_cast<uint32_t>(part); i < p; i += parts)
-        std::memcpy(parity_out[i] + off, ctx->pin_out.p + static_cast<size_t>(i) * S + off, c);
-    });
-  };
-  if (zc) {  // the kernel reads and writes page-locked host memory over PCIe
-    uint8_t *dd, *dp = nullptr;
-    HIP_TRY(ctx, host_dev_ptr(in_direct ? const_cast<uint8_t *>(data) : ctx->pin_in.p, &dd));
-    std::vector<uint8_t *> pd(p);
-    if (out_direct) {
-      for (uint32_t i = 0; i < p; i++) HIP_TRY(ctx, host_dev_ptr(parity_out[i], &pd[i]));
-    } else {
-      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dp));
-      for (uint32_t i = 0; i < p; i++) pd[i] = dp + static_cast<size_t>(i) * S;
-    }
-    auto launch = [&](size_t off, size_t cnt) {
-      for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S + off;
-      for (uint32_t i = 0; i < p; i++) out[i] = pd[i] + off;
-      return encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), cnt, 1, s);
-    };
-    if (in_direct && out_direct) {  // nothing to overlap
-      const int rc = launch(0, S);
-      if (rc) return rc;
-      HIP_TRY(ctx, hipStreamSynchronize(s));
-      return STORB_RS_OK;
-    }
-    return sliced(
-        ctx, S, [&](size_t off, size_t cnt) { if (!in_direct) pack(off, cnt); }, launch,
-        [&](size_t off, size_t cnt) { if (!out_direct) unpack(off, cnt); });
-  }
-  pack(0, S);
-  uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
-  HIP_TRY(ctx, hipMemcpyAsync(dd, ctx->pin_in.p, static_cast<size_t>(k) * S,
-                              hipMemcpyHostToDevice, s));
-  for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
-  for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
-  int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S, 1, s);
-  if (rc) return rc;
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dp, static_cast<size_t>(p) * S,
-                              hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipStreamSynchronize(s));
-  unpack(0, S);
-  return STORB_RS_OK;
-}
-
-int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
-                    const uint32_t *share_idx, uint32_t nshares, size_t block,
-                    size_t padlen, uint8_t *out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
-  if (!shares || !share_idx || !out || block == 0 ||
-      padlen >= static_cast<size_t>(k) * block)
-    return fail(ctx, STORB_RS_EINVAL, "decode: bad arguments");
-  std::vector<uint32_t> slot_idx, slot_pos, missing;
-  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
-  if (rc) return rc;
-  std::vector<uint8_t> coef;
-  rc = decode_rows(ctx, k, n, slot_idx, coef, missing);
-  if (rc) return rc;
-  const size_t outlen = static_cast<size_t>(k) * block - padlen;
-  auto put = [&](uint32_t row, const uint8_t *src) {
-    const size_t off = static_cast<size_t>(row) * block;
-    if (off < outlen) std::memcpy(out + off, src, std::min(block, outlen - off));
-  };
-  HostPool &pool = host_pool(ctx);
-  const int parts = static_cast<size_t>(k) * block >= (1u << 20) ? static_cast<int>(k) : 1;
-  auto put_present = [&] {  // surviving data shares: plain copies into out
-    pool.run(parts, [&](int part) {
-      for (uint32_t s = static_cast<uint32_t>(part); s < k; s += parts)
-        if (slot_idx[s] < k) put(s, shares[slot_pos[s]]);
-    });
-  };
-  if (missing.empty()) {  // all data shares present: concatenation, as zfec
-    put_present();
-    return STORB_RS_OK;
-  }
-  const size_t S = round_up(block, kAlign);
-  const uint32_t e = static_cast<uint32_t>(missing.size());
-  const bool zc = static_cast<size_t>(k + e) * S <= ctx->zc_max;
-  auto aligned = [](const void *q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  // Page-locked, aligned caller shares / output are used in place.
-  bool in_direct = zc && S == block;
-  for (uint32_t c = 0; in_direct && c < k; c++)
-    in_direct = aligned(shares[slot_pos[c]]) && range_pinned(shares[slot_pos[c]], block);
-  const bool out_direct = zc && S == block && padlen == 0 && aligned(out) &&
-                          range_pinned(out, outlen);
-  DeviceGuard g(ctx->device);
-  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(e) * S));
-  if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + e) * S));
-  // columns [off, off + cnt) of row `row` of the chunk (truncated at outlen)
-  auto put_cols = [&](uint32_t row, size_t off, size_t cnt, const uint8_t *src) {
-    const size_t o = static_cast<size_t>(row) * block + off;
-    size_t c = off < block ? std::min(cnt, block - off) : 0;
-    c = o < outlen ? std::min(c, outlen - o) : 0;
-    if (c) std::memcpy(out + o, src, c);
-  };
-  // slot shares into pinned staging; present data shares also into out
-  auto pack = [&](size_t off, size_t cnt) {
-    const int pp = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
-    pool.run(pp, [&](int part) {
-      for (uint32_t c = static_cast<uint32_t>(part); c < k; c += pp) {
-        const uint8_t *src = shares[slot_pos[c]] + off;
-        const size_t avail = off < block ? std::min(cnt, block - off) : 0;
-        if (!in_direct) {
-          uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(c) * S + off;
-          if (avail) std::memcpy(dst, src, avail);
-          if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
-        }
-        if (slot_idx[c] < k) put_cols(c, off, cnt, src);
-      }
-    });
-  };
-  auto unpack = [&](size_t off, size_t cnt) {
-    if (out_direct) return;
-    for (uint32_t r = 0; r < e; r++)
-      put_cols(missing[r], off, cnt, ctx->pin_out.p + static_cast<size_t>(r) * S + off);
-  };
-  hipStream_t s = ctx->stream;
-  std::vector<const uint8_t *> in(k);
-  std::vector<uint8_t *> o(e);
-  std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(e, static_cast<size_t>(e) * S);
-  if (zc) {  // zero-copy: the kernel reads / writes page-locked host memory
-    std::vector<uint8_t *> id(k), od(e);
-    uint8_t *base = nullptr;
-    if (in_direct) {
-      for (uint32_t c = 0; c < k; c++)
-        HIP_TRY(ctx, host_dev_ptr(const_cast<uint8_t *>(shares[slot_pos[c]]), &id[c]));
-    } else {
-      HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &base));
-      for (uint32_t c = 0; c < k; c++) id[c] = base + static_cast<size_t>(c) * S;
-    }
-    if (out_direct) {
-      HIP_TRY(ctx, host_dev_ptr(out, &base));
-      for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(missing[r]) * block;
-    } else {
-      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &base));
-      for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(r) * S;
-    }
-    auto launch = [&](size_t off, size_t cnt) {
-      for (uint32_t c = 0; c < k; c++) in[c] = id[c] + off;
-      for (uint32_t r = 0; r < e; r++) o[r] = od[r] + off;
-      return apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), cnt, 1,
-                   s);
-    };
-    if (in_direct && out_direct) {
-      rc = launch(0, S);
-      if (rc) return rc;
-      put_present();  // host copies overlap the kernel (disjoint rows of out)
-      HIP_TRY(ctx, hipStreamSynchronize(s));
-      return STORB_RS_OK;
-    }
-    return sliced(ctx, S, pack, launch, unpack);
-  }
-  pack(0, S);
-  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
-  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
-                              hipMemcpyHostToDevice, s));
-  for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
-  for (uint32_t r = 0; r < e; r++) o[r] = dout + static_cast<size_t>(r) * S;
-  rc = apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1, s);
-  if (rc) return rc;
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(e) * S,
-                              hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipStreamSynchronize(s));
-  unpack(0, S);
-  return STORB_RS_OK;
-}
-
-int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
-                    const uint32_t *share_idx, uint32_t nshares, size_t block,
-                    const uint32_t *targets, uint32_t ntargets, uint8_t *const *out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
-  if (!shares || !share_idx || (ntargets && (!targets || !out)) || block == 0)
-    return fail(ctx, STORB_RS_EINVAL, "repair: bad arguments");
-  std::vector<uint32_t> slot_idx, slot_pos;
-  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
-  if (rc) return rc;
-  std::vector<uint8_t> coef;
-  rc = repair_rows(ctx, k, n, slot_idx, targets, ntargets, coef);
-  if (rc || ntargets == 0) return rc;
-  const size_t S = round_up(block, kAlign);
-  DeviceGuard g(ctx->device);
-  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(ntargets) * S));
-  HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + ntargets) * S));
-  for (uint32_t c = 0; c < k; c++) {
-    std::memcpy(ctx->pin_in.p + static_cast<size_t>(c) * S, shares[slot_pos[c]], block);
-    std::memset(ctx->pin_in.p + static_cast<size_t>(c) * S + block, 0, S - block);
-  }
-  hipStream_t s = ctx->stream;
-  const bool zc = static_cast<size_t>(k + ntargets) * S <= ctx->zc_max;
-  uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
-  if (zc) {  // zero-copy: the kernel works on the pinned staging directly
-    HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &din));
-    HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dout));
-  } else {
-    HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
-                                hipMemcpyHostToDevice, s));
-  }
-  std::vector<const uint8_t *> in(k);
-  std::vector<uint8_t *> o(ntargets);
-  std::vector<size_t> ins(k, static_cast<size_t>(k) * S),
-      outs(ntargets, static_cast<size_t>(ntargets) * S);
-  for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
-  for (uint32_t r = 0; r < ntargets; r++) o[r] = dout + static_cast<size_t>(r) * S;
-  rc = apply(ctx, k, ntargets, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1,
-             s);
-  if (rc) return rc;
-  if (!zc)
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(ntargets) * S,
-                                hipMemcpyDeviceToHost, s));
-  HIP_TRY(ctx, hipStreamSynchronize(s));
-  for (uint32_t r = 0; r < ntargets; r++)
-    std::memcpy(out[r], ctx->pin_out.p + static_cast<size_t>(r) * S, block);
-  return STORB_RS_OK;
-}
-
-// Pipelined batch encode: two pinned in/out buffer pairs and two streams.
-// While the GPU copies and encodes batch i, the host packs batch i+1 and
-// unpacks batch i-1 (hipMemcpyAsync from pinned memory is a true DMA).
-// With hashes_out, the blake3 of every share is computed on the device
-// right after the encode kernel and only the digests come back.
-static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
-                              const uint8_t *data, size_t chunk_len, uint32_t nchunks,
-                              uint8_t *parity_out, uint8_t *hashes_out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
-  if (chunk_len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
-  const uint32_t p = n - k;
-  if (nchunks == 0) return STORB_RS_OK;
-  if (p > 0 && !parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
-  const size_t B = (chunk_len + k - 1) / k;
-  if (hashes_out && B > 16ull * 1024 * 1024)
-    return fail(ctx, STORB_RS_EINVAL, "blake3: share larger than 16 MiB");
-  const size_t S = round_up(B, kAlign);
-  const bool packed = (S == B) && (B * k == chunk_len);
-  // ~64 MiB of input per batch keeps both DMA directions busy.
-  const size_t per = static_cast<size_t>(k) * S;
-  uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
-  batch = std::min(batch, nchunks);
-  const size_t hash_bytes = hashes_out ? static_cast<size_t>(batch) * n * 32 : 0;
-  // Caller buffers that are page-locked (storb_rs_host_alloc / _register)
-  // are DMA'd directly: no pack copy in, no unpack copy out.
-  const bool in_direct = packed && range_pinned(data, static_cast<size_t>(nchunks) * chunk_len);
-  const bool out_direct =
-      p > 0 && S == B && range_pinned(parity_out, static_cast<size_t>(nchunks) * p * B);
-  // Page-locked caller chunks without piece ids: the kernel reads them (and
-  // writes parity) over PCIe directly (zero-copy). Kernel-driven PCIe
-  // traffic overlaps both directions, where the SDMA copies of H2D and D2H
-  // share one ceiling (57 GB/s total, tools/pcie_probe.py): 47 vs 35 GiB/s
-  // measured. From pageable chunks the SDMA pipeline stays ahead (34 vs
-  // 20 GiB/s: the host's packing competes with the kernel's reads of the
-  // same staging), and the hashed path keeps the shares on the device.
-  const bool zc = ctx->zc_batch && !hashes_out && p > 0 && in_direct;
-  DeviceGuard g(ctx->device);
-  for (int b = 0; b < 2; b++) {
-    if (!in_direct) HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
-    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(p) * S * batch + hash_bytes));
-    if (!zc)
-      HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
-  }
-  const uint32_t nb = (nchunks + batch - 1) / batch;
-  HostPool &pool = host_pool(ctx);
-  auto unpack = [&](uint32_t bi) {
-    const int b = bi & 1;
-    const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
-    if (p > 0 && !out_direct) {
-      if (S == B) {
-        pool.copy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
-                  static_cast<size_t>(cn) * p * B);
-      } else {
-        pool.run(static_cast<int>(cn), [&](int c) {
-          for (uint32_t i = 0; i < p; i++)
-            std::memcpy(parity_out + ((static_cast<size_t>(c0) + c) * p + i) * B,
-                        ctx->pipe_out[b].p + (static_cast<size_t>(c) * p + i) * S, B);
-        });
-      }
-    }
-    if (hashes_out) {
-      // device order: [c][j] data digests, then [c][i] parity digests
-      const uint8_t *hd = ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch;
-      const uint8_t *hp = hd + static_cast<size_t>(cn) * k * 32;
-      for (uint32_t c = 0; c < cn; c++) {
-        uint8_t *o = hashes_out + (static_cast<size_t>(c0) + c) * n * 32;
-        std::memcpy(o, hd + static_cast<size_t>(c) * k * 32, static_cast<size_t>(k) * 32);
-        std::memcpy(o + static_cast<size_t>(k) * 32, hp + static_cast<size_t>(c) * p * 32,
-                    static_cast<size_t>(p) * 32);
-      }
-    }
-  };
-  for (uint32_t bi = 0; bi < nb; bi++) {
-    const int b = bi & 1;
-    hipStream_t s = ctx->pipe[b];
-    // Pinned buffer pair b is free once batch bi-2 has landed (device
-    // buffers are reused in stream order and need no host wait).
-    if (bi >= 2 && !(in_direct && (out_direct || p == 0) && !hashes_out)) {
-      HIP_TRY(ctx, hipStreamSynchronize(s));
-      unpack(bi - 2);
-    }
-    const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
-    const uint8_t *hin = in_direct ? data + static_cast<size_t>(c0) * chunk_len
-                                   : ctx->pipe_in[b].p;
-    if (in_direct) {
-      // the H2D below reads the caller's page-locked chunks in place
-    } else if (packed) {
-      pool.copy(ctx->pipe_in[b].p, data + static_cast<size_t>(c0) * chunk_len, per * cn);
-    } else {
-      pool.run(static_cast<int>(cn), [&](int c) {
-        const uint8_t *src = data + (static_cast<size_t>(c0) + c) * chunk_len;
-        for (uint32_t j = 0; j < k; j++) {
-          const size_t off = static_cast<size_t>(j) * B;
-          const size_t cnt = off < chunk_len ? std::min(B, chunk_len - off) : 0;
-          uint8_t *dst = ctx->pipe_in[b].p + static_cast<size_t>(c) * per +
-                         static_cast<size_t>(j) * S;
-          if (cnt) std::memcpy(dst, src + off, cnt);
-          std::memset(dst + cnt, 0, S - cnt);
-        }
-      });
-    }
-    if (zc) {  // the kernel reads the pinned chunks and writes pinned parity over PCIe
-      uint8_t *di, *dq;
-      HIP_TRY(ctx, host_dev_ptr(const_cast<uint8_t *>(hin), &di));
-      HIP_TRY(ctx, host_dev_ptr(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
-                                           : ctx->pipe_out[b].p,
-                                &dq));
-      std::vector<const uint8_t *> in(k);
-      std::vector<uint8_t *> out(p);
-      std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
-      for (uint32_t j = 0; j < k; j++) in[j] = di + static_cast<size_t>(j) * S;
-      for (uint32_t i = 0; i < p; i++) out[i] = dq + static_cast<size_t>(i) * S;
-      const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S,
-                                  cn, s);
-      if (rc) return rc;
-      continue;
-    }
-    uint8_t *dd = ctx->pipe_dev[b].p;
-    uint8_t *dp = dd + per * batch;
-    uint8_t *dh = dp + static_cast<size_t>(p) * S * batch;  // digests (if any)
-    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
-    if (p > 0) {
-      std::vector<const uint8_t *> in(k);
-      std::vector<uint8_t *> out(p);
-      std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
-      for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
-      for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
-      const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S,
-                                  cn, s);
-      if (rc) return rc;
-    }
-    size_t back = static_cast<size_t>(p) * S * cn;
-    if (hashes_out) {
-      // shares are pitched S apart across the whole batch: one launch each
-      HIP_TRY(ctx, launch_blake3_batch(dd, B, cn * k, S, dh, s));
-      if (p > 0)
-        HIP_TRY(ctx, launch_blake3_batch(dp, B, cn * p, S, dh + static_cast<size_t>(cn) * k * 32,
-                                         s));
-    }
-    if (back)
-      HIP_TRY(ctx, hipMemcpyAsync(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
-                                             : ctx->pipe_out[b].p,
-                                  dp, back, hipMemcpyDeviceToHost, s));
-    if (hashes_out)
-      HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch, dh,
-                                  static_cast<size_t>(cn) * n * 32, hipMemcpyDeviceToHost, s));
-  }
-  for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[bi & 1]));
-    unpack(bi);
-  }
-  return STORB_RS_OK;
-}
-
-// Pipelined batch decode (the download path, download.rs:453-465, one
-// chunk after another today). Every chunk selects its first k shares by
-// index (decode_chunk, piece.rs:368-381). Chunks whose k data shares are all
-// present are pure host copies; the rest are grouped by erasure pattern, so
-// each batch is one launch of one decode matrix, and stream through the same
-// double-buffered pinned pipeline as encode: pack the k survivors into
-// pinned staging (present data shares also go straight to `out`), H2D,
-// rebuild only the missing rows, D2H them, unpack into `out`.
-int storb_rs_decode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
-                           size_t padlen, uint32_t nchunks, const uint8_t *const *shares,
-                           const uint32_t *share_idx, const uint32_t *nshares, uint8_t *out,
-                           size_t out_stride) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
-  if (nchunks == 0) return STORB_RS_OK;
-  if (!shares || !share_idx || !nshares || !out || block == 0 ||
-      padlen >= static_cast<size_t>(k) * block)
-    return fail(ctx, STORB_RS_EINVAL, "decode_chunks: bad arguments");
-  const size_t outlen = static_cast<size_t>(k) * block - padlen;
-  if (out_stride == 0) out_stride = outlen;
-  if (out_stride < outlen) return fail(ctx, STORB_RS_EINVAL, "decode_chunks: out_stride < chunk");
-  // per chunk: its k slot shares (pointers) and erasure pattern
-  std::vector<const uint8_t *> slot_ptr(static_cast<size_t>(nchunks) * k);
-  std::map<std::vector<uint32_t>, std::vector<uint32_t>> groups;
-  std::vector<uint32_t> plain;
-  size_t off = 0;
-  for (uint32_t c = 0; c < nchunks; c++) {
-    std::vector<uint32_t> slot_idx, slot_pos;
-    const int rc = select_shares(ctx, k, n, share_idx + off, nshares[c], slot_idx, slot_pos);
-    if (rc) {
-      ctx->last_error += " (chunk " + std::to_string(c) + ")";
-      return rc;
-    }
-    for (uint32_t s = 0; s < k; s++) {
-      slot_ptr[static_cast<size_t>(c) * k + s] = shares[off + slot_pos[s]];
-      if (!slot_ptr[static_cast<size_t>(c) * k + s])
-        return fail(ctx, STORB_RS_EINVAL, "decode_chunks: null share");
-    }
-    off += nshares[c];
-    bool all_data = true;
-    for (uint32_t s = 0; s < k; s++) all_data &= slot_idx[s] == s;
-    if (all_data)
-      plain.push_back(c);
-    else
-      groups[slot_idx].push_back(c);
-  }
-  HostPool &pool = host_pool(ctx);
-  auto put_row = [&](uint32_t c, uint32_t row, const uint8_t *src) {
-    const size_t o = static_cast<size_t>(row) * block;
-    if (o < outlen)
-      std::memcpy(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
-  };
-  if (!plain.empty())  // all data shares present: concatenation (zfec does the same)
-    pool.run(static_cast<int>(plain.size()), [&](int i) {
-      for (uint32_t s = 0; s < k; s++)
-        put_row(plain[i], s, slot_ptr[static_cast<size_t>(plain[i]) * k + s]);
-    });
-  if (groups.empty()) return STORB_RS_OK;
-
-  struct Item {
-    const std::vector<uint32_t> *slots;
-    const uint32_t *chunks;
-    uint32_t cn;
-    std::vector<uint8_t> coef;
-    std::vector<uint32_t> missing;
-  };
-  const size_t S = round_up(block, kAlign);
-  const size_t per = static_cast<size_t>(k) * S;
-  uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
-  std::vector<Item> items;
-  uint32_t emax = 0;
-  for (auto &g : groups) {
-    std::vector<uint8_t> coef;
-    std::vector<uint32_t> missing;
-    const int rc = decode_rows(ctx, k, n, g.first, coef, missing);
-    if (rc) return rc;
-    emax = std::max<uint32_t>(emax, static_cast<uint32_t>(missing.size()));
-    for (size_t i = 0; i < g.second.size(); i += batch)
-      items.push_back(Item{&g.first, g.second.data() + i,
-                           static_cast<uint32_t>(std::min<size_t>(batch, g.second.size() - i)),
-                           coef, missing});
-  }
-  batch = 0;
-  for (auto &it : items) batch = std::max(batch, it.cn);
-  DeviceGuard dg(ctx->device);
-  for (int b = 0; b < 2; b++) {
-    HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
-    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(emax) * S * batch));
-    HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(k + emax) * S * batch));
-  }
-  auto unpack = [&](size_t ii) {
-    const Item &it = items[ii];
-    const uint8_t *src = ctx->pipe_out[ii & 1].p;
-    const uint32_t e = static_cast<uint32_t>(it.missing.size());
-    pool.run(static_cast<int>(it.cn), [&](int c) {
-      for (uint32_t r = 0; r < e; r++)
-        put_row(it.chunks[c], it.missing[r], src + (static_cast<size_t>(c) * e + r) * S);
-    });
-  };
-  for (size_t ii = 0; ii < items.size(); ii++) {
-    const int b = ii & 1;
-    hipStream_t s = ctx->pipe[b];
-    if (ii >= 2) {  // pinned pair b is free once item ii-2 has landed
-      HIP_TRY(ctx, hipStreamSynchronize(s));
-      unpack(ii - 2);
-    }
-    const Item &it = items[ii];
-    const uint32_t e = static_cast<uint32_t>(it.missing.size());
-    uint8_t *hin = ctx->pipe_in[b].p;
-    pool.run(static_cast<int>(it.cn), [&](int c) {
-      const uint32_t ch = it.chunks[c];
-      for (uint32_t sl = 0; sl < k; sl++) {
-        const uint8_t *src = slot_ptr[static_cast<size_t>(ch) * k + sl];
-        uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(sl) * S;
-        std::memcpy(dst, src, block);
-        if (S > block) std::memset(dst + block, 0, S - block);
-        if ((*it.slots)[sl] == sl) put_row(ch, sl, src);  // present data share
-      }
-    });
-    uint8_t *dd = ctx->pipe_dev[b].p;
-    uint8_t *dm = dd + per * it.cn;
-    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * it.cn, hipMemcpyHostToDevice, s));
-    std::vector<const uint8_t *> in(k);
-    std::vector<uint8_t *> o(e);
-    std::vector<size_t> ins(k, per), outs(e, static_cast<size_t>(e) * S);
-    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
-    for (uint32_t r = 0; r < e; r++) o[r] = dm + static_cast<size_t>(r) * S;
-    const int rc = apply(ctx, k, e, it.coef.data(), in.data(), ins.data(), o.data(), outs.data(),
-                         S, it.cn, s);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(e) * S * it.cn,
-                                hipMemcpyDeviceToHost, s));
-  }
-  for (size_t ii = items.size() >= 2 ? items.size() - 2 : 0; ii < items.size(); ii++) {
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[ii & 1]));
-    unpack(ii);
-  }
-  return STORB_RS_OK;
-}
-
-int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
-                           size_t chunk_len, uint32_t nchunks, uint8_t *parity_out) {
-  return encode_chunks_impl(ctx, k, n, data, chunk_len, nchunks, parity_out, nullptr);
-}
-
-int storb_rs_encode_chunks_hashed(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
-                                  const uint8_t *data, size_t chunk_len, uint32_t nchunks,
-                                  uint8_t *parity_out, uint8_t *hashes_out) {
-  if (!hashes_out) return STORB_RS_EINVAL;
-  return encode_chunks_impl(ctx, k, n, data, chunk_len, nchunks, parity_out, hashes_out);
 }
 
 }  // extern "C"
