@@ -3,6 +3,12 @@
 There is no fallback: if the HIP library is missing, importing this module
 raises. Host-only entry points (sizing, generator matrix, parameter checks)
 work without a GPU; every compute entry point needs a gfx950 device.
+
+With PyTorch in the same process, import torch before this library is
+loaded: PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so,
+ROCm 7.0) beside the image's /opt/rocm 7.2 one linked here. The two coexist
+when torch's is loaded first; the other way round torch finds no GPU
+("No HIP GPUs are available"). bench.py, smoke() and tests/conftest.py do so.
 """
 from __future__ import annotations
 
@@ -109,16 +115,6 @@ def lib():
                         f"{LIB_PATH} is missing: the MI355X library must be built "
                         "(python -c 'import __graft_entry__ as g; g.build()'); there is "
                         "no CPU fallback")
-                # PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so,
-                # ROCm 7.0) beside the image's /opt/rocm 7.2 one this library links.
-                # Both coexist when torch's is initialised first; loaded the other
-                # way round torch finds no GPU (observed: "No HIP GPUs are
-                # available"). Callers that pass torch device pointers therefore
-                # get torch loaded first; without torch nothing changes.
-                try:
-                    import torch  # noqa: F401
-                except ImportError:
-                    pass
                 L = C.CDLL(LIB_PATH)
                 _declare(L)
                 _lib = L

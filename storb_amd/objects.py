@@ -119,11 +119,12 @@ def encode_object(data, ctx: Optional[_lib.Context] = None) -> EncodedObject:
 
 
 def reconstruct_object(chunks: Sequence[ChunkValue], fetched: Sequence[Dict[int, bytes]],
-                       ctx: Optional[_lib.Context] = None) -> bytes:
+                       ctx: Optional[_lib.Context] = None) -> np.ndarray:
     """The download side: fetched[c] maps piece_idx -> piece bytes of chunk c
     (any subset); each chunk rebuilds from its first k pieces by index
     (reconstruct_chunk); PieceError if a chunk has fewer than k. One batched
-    GPU call per run of chunks of one geometry."""
+    GPU call per run of chunks of one geometry. Returns the object's bytes
+    as a uint8 array (no extra copy into a bytes object)."""
     ctx = ctx or _lib.thread_context()
     for ci, (cv, got) in enumerate(zip(chunks, fetched)):
         if len(got) < cv.k:
@@ -145,4 +146,4 @@ def reconstruct_object(chunks: Sequence[ChunkValue], fetched: Sequence[Dict[int,
         ctx.decode_chunks(k, m, B, pad, batch, out=out[off:off + (j - i) * ln].reshape(j - i, ln))
         off += (j - i) * ln
         i = j
-    return out.tobytes()
+    return out

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# torch's own HIP runtime must be loaded before libstorb_rs.so's (see the
+# storb_amd/_lib.py docstring); CPU-only test modules may load the library
+# first otherwise, and a later torch.cuda call then finds no GPU.
+import torch  # noqa: F401  (before any storb_amd import)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 

@@ -41,7 +41,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-from storb_amd import _lib, partition, wire  # noqa: E402
+from storb_amd import _lib, objects, wire  # noqa: E402
 
 GIB = float(1 << 30)
 HANDSHAKE = bytes(96)  # opaque HandshakePayload bytes (auth out of scope)
@@ -149,41 +149,24 @@ def _run(a, miners):
     M = len(miners)
     ctx = _lib.Context(-1)
     obj = splitmix_bytes(0x5709B + a.seed, a.size)
-    chunk_size = _lib.piece_length(a.size)
-    chunks = partition.chunks_of(a.size, chunk_size)
+    chunks = objects.chunk_spans(a.size)
+    chunk_size = chunks[0][1]
     metas = []  # per chunk: k, m, B, padlen, piece hashes, miner per piece
 
-    # ---- upload: GPU encode + GPU piece ids, then the store framing
+    # ---- upload: GPU encode + GPU piece ids (objects.encode_object: one
+    # batched call per run of equal chunks), then the store framing
     t0 = time.perf_counter()
-    groups = {}
-    for ci, (off, ln) in enumerate(chunks):
-        groups.setdefault(ln, []).append(ci)
-    parity_of, hashes_of = {}, {}
-    for ln, idxs in groups.items():
-        k, n = _lib.get_k_and_m(ln)
-        lo = idxs[0]
-        assert idxs == list(range(lo, lo + len(idxs)))
-        par, hashes = ctx.encode_chunks_hashed(k, n, obj[lo * chunk_size:lo * chunk_size +
-                                                          len(idxs) * ln], ln, len(idxs))
-        B = _lib.block_size(k, ln)
-        par = par.reshape(len(idxs), n - k, B)
-        for j, ci in enumerate(idxs):
-            parity_of[ci], hashes_of[ci] = par[j], hashes[j]
+    enc = objects.encode_object(obj, ctx)
     t_encode = time.perf_counter() - t0
 
     per_miner = [[] for _ in range(M)]
-    for ci, (off, ln) in enumerate(chunks):
-        k, n = _lib.get_k_and_m(ln)
-        B = _lib.block_size(k, ln)
-        padded = obj[off:off + ln]
-        if B * k != ln:
-            padded = np.concatenate([padded, np.zeros(B * k - ln, dtype=np.uint8)])
-        metas.append({"k": k, "m": n, "B": B, "padlen": B * k - ln, "off": off, "len": ln,
-                      "hashes": [hashes_of[ci][i].tobytes() for i in range(n)],
+    for ci, ((off, ln), cv, pv, sh) in enumerate(zip(chunks, enc.chunks, enc.pieces, enc.data)):
+        n = cv.m
+        metas.append({"k": cv.k, "m": n, "B": cv.chunk_size, "padlen": cv.padlen, "off": off,
+                      "len": ln, "hashes": [p.piece_hash for p in pv],
                       "miner": [(ci * n + i) % M for i in range(n)]})
         for i in range(n):
-            piece = padded[i * B:(i + 1) * B] if i < k else parity_of[ci][i - k]
-            per_miner[(ci * n + i) % M].append((ci, i, piece))
+            per_miner[(ci * n + i) % M].append((ci, i, sh[i]))
 
     def upload(m):
         s = socket.create_connection(("127.0.0.1", miners[m]["store"]))
@@ -243,32 +226,16 @@ def _run(a, miners):
         gathered = dict(ex.map(gather, range(len(chunks))))
     t_fetch = time.perf_counter() - t1
 
-    out = np.empty(a.size, dtype=np.uint8)
     needed_parity = 0
+    for ci, meta in enumerate(metas):
+        if len(gathered[ci]) < meta["k"]:
+            raise SystemExit(f"chunk {ci}: not enough pieces ({len(gathered[ci])} < {meta['k']})")
+        needed_parity += any(i >= meta["k"] for i in sorted(gathered[ci])[:meta["k"]])
     t2 = time.perf_counter()
-    # Consecutive chunks of one geometry (all but a short tail) reconstruct in
-    # one storb_rs_decode_chunks call straight into the object buffer; each
-    # chunk keeps decode_chunk's own first-k-by-index choice.
-    runs, ci = [], 0
-    while ci < len(metas):
-        geo = tuple(metas[ci][x] for x in ("k", "m", "B", "padlen", "len"))
-        cj = ci
-        while cj < len(metas) and tuple(metas[cj][x] for x in ("k", "m", "B", "padlen", "len")) == geo:
-            cj += 1
-        runs.append((ci, cj))
-        ci = cj
-    for c0, c1 in runs:
-        meta = metas[c0]
-        batch = []
-        for ci in range(c0, c1):
-            got = gathered[ci]
-            if len(got) < meta["k"]:
-                raise SystemExit(f"chunk {ci}: not enough pieces ({len(got)} < {meta['k']})")
-            ids = sorted(got)
-            needed_parity += any(i >= meta["k"] for i in ids[:meta["k"]])
-            batch.append(([got[i] for i in ids], ids))
-        view = out[meta["off"]:meta["off"] + (c1 - c0) * meta["len"]].reshape(c1 - c0, meta["len"])
-        ctx.decode_chunks(meta["k"], meta["m"], meta["B"], meta["padlen"], batch, out=view)
+    # reconstruct_chunk per chunk (first k by index), batched per run of
+    # equal chunks straight into the object buffer
+    out = objects.reconstruct_object(enc.chunks, [gathered[ci] for ci in range(len(metas))],
+                                     ctx)
     t_decode = time.perf_counter() - t2
     t_download = time.perf_counter() - t1
     ok = bool(np.array_equal(out, obj))
