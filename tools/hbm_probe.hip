@@ -299,6 +299,21 @@ int main(int argc, char **argv) {
   ADDW(8, true, 2);
   ADDW(8, false, 2);
 
+  // wide stripes (Storb's k = 16 geometry): a quarter of the stripes, same bytes
+  const Args a16{in, out, sink, B, NS / 4};
+  const uint32_t grid16 = static_cast<uint32_t>((NS / 4) * (B / 16 / T));
+#define ADD16(KI, RO)                                                                          \
+  vs.push_back(Variant{std::string("wide KI=") + #KI + " RO=" + #RO + " nt/nt",                 \
+                       static_cast<double>(NS / 4) * ((KI) + (RO)) * B,                       \
+                       [=](hipStream_t s) {                                                    \
+                         hipLaunchKernelGGL((probe<KI, RO, 2, 2, false, T>), dim3(grid16),     \
+                                            dim3(T), 0, s, a16);                               \
+                       },                                                                      \
+                       {}})
+  ADD16(16, 2);
+  ADD16(16, 8);
+  ADD16(8, 4);
+  ADD16(8, 3);
   vs.push_back(Variant{"xcd-remapped KI=4 RO=2 nt/nt", static_cast<double>(NS) * 6 * B,
                        [=](hipStream_t s) {
                          hipLaunchKernelGGL((probe_xcd<true, T>), dim3(grid), dim3(T), 0, s, a);
