@@ -201,6 +201,30 @@ __global__ __launch_bounds__(T) void probe_xcd(const Args a) {
   }
 }
 
+// Wide shapes with U columns per lane (U x 4 KiB of every share per
+// workgroup): does a longer run per stream help when 16+ streams interleave?
+template <int KI, int RO, int U, int T>
+__global__ __launch_bounds__(T) void probe_u(const Args a) {
+  const uint32_t cols = static_cast<uint32_t>(a.B >> 4);
+  const uint32_t tps = cols / (T * U);
+  const uint32_t stripe = blockIdx.x / tps, tile = blockIdx.x % tps;
+  const u32x4 *in = reinterpret_cast<const u32x4 *>(a.in + static_cast<uint64_t>(stripe) * KI * a.B);
+  u32x4 *out = reinterpret_cast<u32x4 *>(a.out + static_cast<uint64_t>(stripe) * RO * a.B);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t c = tile * T * U + u * T + threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < KI; j++) acc ^= __builtin_nontemporal_load(in + j * cols + c);
+#pragma unroll
+    for (int i = 0; i < RO; i++) {
+      u32x4 o = acc;
+      o.x ^= i;
+      __builtin_nontemporal_store(o, out + i * cols + c);
+    }
+  }
+}
+
 struct Variant {
   std::string name;
   double bytes;
@@ -310,6 +334,18 @@ int main(int argc, char **argv) {
                                             dim3(T), 0, s, a16);                               \
                        },                                                                      \
                        {}})
+#define ADDU(KI, RO, U)                                                                        \
+  vs.push_back(Variant{std::string("wide KI=") + #KI + " RO=" + #RO + " U=" + #U,               \
+                       static_cast<double>(NS / 4) * ((KI) + (RO)) * B,                       \
+                       [=](hipStream_t s) {                                                    \
+                         hipLaunchKernelGGL((probe_u<KI, RO, U, T>), dim3(grid16 / (U)),       \
+                                            dim3(T), 0, s, a16);                               \
+                       },                                                                      \
+                       {}})
+  ADDU(16, 2, 1);
+  ADDU(16, 2, 2);
+  ADDU(16, 2, 4);
+  ADDU(16, 8, 2);
   ADD16(16, 2);
   ADD16(16, 8);
   ADD16(8, 4);
