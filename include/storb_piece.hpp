@@ -21,6 +21,7 @@
 #pragma once
 
 #include <cstdint>
+#include <array>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -149,6 +150,12 @@ std::vector<uint8_t> decode_chunk(const EncodedChunk &encoded_chunk);
 std::vector<uint8_t> reconstruct_data(const std::vector<Piece> &pieces,
                                       const std::vector<EncodedChunk> &chunks);
 Result<std::vector<uint8_t>, PieceError> reconstruct_chunk(const EncodedChunk &chunk);
+
+// piece.rs:257-276: blake3(owner account id || piece hashes...), the
+// object's InfoHash (upload.rs:292). 32-byte hashes in, 32 bytes out.
+std::array<uint8_t, 32> get_infohash_by_identity(
+    const std::vector<std::array<uint8_t, 32>> &piece_hashes,
+    const std::vector<uint8_t> &owner_account_id);
 
 }  // namespace piece
 }  // namespace storb

@@ -207,5 +207,15 @@ Result<std::vector<uint8_t>, PieceError> reconstruct_chunk(const EncodedChunk &c
   return R::Ok(decode_chunk(to_decode));
 }
 
+std::array<uint8_t, 32> get_infohash_by_identity(
+    const std::vector<std::array<uint8_t, 32>> &piece_hashes,
+    const std::vector<uint8_t> &owner_account_id) {
+  std::vector<uint8_t> msg(owner_account_id);
+  for (const auto &h : piece_hashes) msg.insert(msg.end(), h.begin(), h.end());
+  std::array<uint8_t, 32> out{};
+  storb_blake3(msg.data(), msg.size(), out.data());
+  return out;
+}
+
 }  // namespace piece
 }  // namespace storb

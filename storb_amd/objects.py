@@ -27,7 +27,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from .piece import PieceError, PieceType
+from .piece import PieceError, PieceType, get_infohash_by_identity  # noqa: F401 (re-export)
 
 
 @dataclass
@@ -69,11 +69,6 @@ def chunk_spans(total: int) -> List[Tuple[int, int]]:
         return []
     size = _lib.piece_length(total)
     return [(o, min(size, total - o)) for o in range(0, total, size)]
-
-
-def get_infohash_by_identity(piece_hashes: Sequence[bytes], owner_account_id: bytes) -> bytes:
-    """piece.rs:257-276: blake3(owner account id || piece hashes...)."""
-    return _lib.blake3(bytes(owner_account_id) + b"".join(bytes(h) for h in piece_hashes))
 
 
 def _runs(spans: Sequence[Tuple[int, int]]):

@@ -3,8 +3,8 @@
 Same names, argument meaning and error behaviour as the reference:
 ``piece_length`` (piece.rs:292-303), ``get_k_and_m`` (:307-317),
 ``encode_chunk`` (:320-361), ``decode_chunk`` (:363-387),
-``reconstruct_data`` (:389-438), ``reconstruct_chunk`` (:441-481) and the
-carrier types (:157-213). Rust ``.expect()`` panics raise :class:`Panic`;
+``reconstruct_data`` (:389-438), ``reconstruct_chunk`` (:441-481),
+``get_infohash_by_identity`` (:257-276) and the carrier types (:157-213). Rust ``.expect()`` panics raise :class:`Panic`;
 ``Result::Err(PieceError)`` raises :class:`PieceError`.
 The C++ mirror of the same file is include/storb_piece.hpp.
 """
@@ -126,3 +126,8 @@ def reconstruct_chunk(chunk: EncodedChunk) -> bytes:
     if len(relevant) < chunk.k:
         raise PieceError(chunk.chunk_idx, chunk.k, len(relevant))
     return decode_chunk(replace(chunk, pieces=relevant))
+
+
+def get_infohash_by_identity(piece_hashes: Sequence[bytes], owner_account_id: bytes) -> bytes:
+    """piece.rs:257-276: blake3(owner account id || piece hashes...)."""
+    return _lib.blake3(bytes(owner_account_id) + b"".join(bytes(h) for h in piece_hashes))

@@ -174,6 +174,21 @@ static void test_threads() {
   for (int v : ok) CHECK(v == 1);
 }
 
+// get_infohash_by_identity (piece.rs:257-276) on a fixed input; the expected
+// digest is blake3(owner || hashes) from the restated reference
+// (oracle/blake3_ref.py), itself pinned to the published vectors.
+static void test_infohash() {
+  std::vector<uint8_t> owner(32);
+  for (int i = 0; i < 32; i++) owner[i] = static_cast<uint8_t>(i);
+  std::vector<std::array<uint8_t, 32>> hs(3);
+  for (int i = 0; i < 3; i++) hs[i].fill(static_cast<uint8_t>(i));
+  const auto got = get_infohash_by_identity(hs, owner);
+  static const char *want = "2efb6fabb62a24e9d0690fb306c6ba2c234085b6352c1e41cc981d075caffa2d";
+  char hex[65];
+  for (int i = 0; i < 32; i++) std::snprintf(hex + 2 * i, 3, "%02x", got[i]);
+  CHECK(std::string(hex) == want);
+}
+
 int main() {
   test_piece_length();
   test_encode_decode_chunk();
@@ -184,6 +199,7 @@ int main() {
   test_reconstruct_single_chunk();
   test_fec_kats_appendix_b();
   test_threads();
+  test_infohash();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;
