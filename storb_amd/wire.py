@@ -103,6 +103,7 @@ class ObjectStore:
 
     def write(self, hexhash: str, data) -> str:
         f = self._file(hexhash)
+        os.makedirs(os.path.dirname(f), exist_ok=True)  # store.rs:50-53
         with open(f, "wb") as fh:
             fh.write(data)
         return f

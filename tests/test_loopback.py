@@ -42,6 +42,30 @@ def test_piece_response_format():
         wire.deserialise_piece_response(wire.serialise_piece_response(h, b"xyw"), h)
 
 
+def test_object_store_mirrors_reference_tests(tmp_path):
+    """crates/storb_miner/src/store.rs:70-182: creating a store (fresh and
+    existing directory), writing a piece to <hash[0:2]>/<hash[2:]> (the
+    folder is created if an existing store lacks it), reading it back,
+    overwriting it."""
+    p = str(tmp_path / "store")
+    s = wire.ObjectStore(p)
+    assert os.path.isdir(p)
+    s2 = wire.ObjectStore(p)  # existing directory
+    assert os.path.isdir(s2.path)
+    bare = tmp_path / "bare"
+    bare.mkdir()
+    wire.ObjectStore(str(bare)).write("ab" + "0" * 62, b"x")  # no hex folders yet
+    assert (bare / "ab" / ("0" * 62)).read_bytes() == b"x"
+    data = os.urandom(1000)
+    hx = ref(data).hex()
+    f = s.write(hx, data)
+    assert f == os.path.join(p, hx[:2], hx[2:]) and os.path.exists(f)
+    assert s.read(hx) == data
+    data2 = os.urandom(1000)
+    s.write(hx, data2)
+    assert s.read(hx) == data2 and s.read(hx) != data
+
+
 def test_miner_store_and_retrieve(tmp_path):
     sp, hp = free_port(), free_port()
     store = tmp_path / "m0"
