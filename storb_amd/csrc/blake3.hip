@@ -176,27 +176,38 @@ __device__ __forceinline__ void store_hash(uint8_t *o, const uint32_t *cv) {
 }
 
 __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
-    const uint8_t *in, uint64_t len, uint64_t stride, uint8_t *out, uint32_t q_log2,
-    uint32_t depth) {
+    const uint8_t *in, uint64_t len, uint64_t stride, uint8_t *out, uint32_t count,
+    uint32_t q_log2, uint32_t depth, uint32_t seg_log2) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds3[];
-  const uint8_t *p = in + static_cast<uint64_t>(blockIdx.x) * stride;
-  uint8_t *o = out + static_cast<uint64_t>(blockIdx.x) * 32;
-  const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
+  // A segment of L = 2^seg_log2 lanes hashes one shard; a workgroup holds
+  // T / L segments (small shards pack several to a workgroup, large ones
+  // take the whole workgroup, L = T).
+  const int T = blockDim.x;
   const int lane = threadIdx.x;
+  const int L = 1 << seg_log2;
+  const int ls = lane & (L - 1), sbase = lane - ls;
+  const uint32_t shard_raw = blockIdx.x * static_cast<uint32_t>(T >> seg_log2) +
+                             static_cast<uint32_t>(lane >> seg_log2);
+  const bool live = shard_raw < count;
+  // Segments past the last shard redo the last one (every lane must reach
+  // the barriers below) and store nothing.
+  const uint32_t shard = live ? shard_raw : count - 1;
+  const uint8_t *p = in + static_cast<uint64_t>(shard) * stride;
+  uint8_t *o = out + static_cast<uint64_t>(shard) * 32;
+  const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(p)) & 15) == 0;
-  if (n == 1) {  // single chunk: it is the root
-    if (lane == 0) {
+  if (n == 1) {  // single chunk: it is the root (one lane per shard, L = 1)
+    if (ls == 0 && live) {
       uint32_t cv[8];
       chunk_cv_dev(cv, p, static_cast<uint32_t>(len), 0, b3::kRoot, aligned16);
       store_hash(o, cv);
     }
     return;
   }
-  const int T = blockDim.x;
   uint32_t *stack = lds3;                          // [depth][8][T]
   uint32_t *nodes = lds3 + depth * 8 * T;          // [2][8][T]
   const uint64_t q = 1ull << q_log2;
-  const uint64_t c0 = static_cast<uint64_t>(lane) * q;
+  const uint64_t c0 = static_cast<uint64_t>(ls) * q;
   const uint64_t c1 = c0 + q < n ? c0 + q : n;
   uint32_t cv[8], left[8];
   int sp = 0;
@@ -234,30 +245,32 @@ __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
     put(nodes, 0, lane, cv, T);
   }
   __syncthreads();
+  // Group nodes merge pairwise within each segment (odd node carried); every
+  // segment has the same count, so the loop is uniform across the block.
   uint32_t cnt = static_cast<uint32_t>((n + q - 1) / q);  // >= 2 by the choice of q
   int cur = 0;
   while (cnt > 2) {
     const uint32_t half = cnt / 2;
     uint32_t *src = nodes + cur * 8 * T, *dst = nodes + (cur ^ 1) * 8 * T;
-    if (static_cast<uint32_t>(lane) < half) {
+    if (static_cast<uint32_t>(ls) < half) {
       uint32_t r[8];
-      get(src, 0, 2 * lane, left, T);
-      get(src, 0, 2 * lane + 1, r, T);
+      get(src, 0, sbase + 2 * ls, left, T);
+      get(src, 0, sbase + 2 * ls + 1, r, T);
       parent_dev(cv, left, r, 0);
       put(dst, 0, lane, cv, T);
-    } else if ((cnt & 1) && static_cast<uint32_t>(lane) == half) {
-      get(src, 0, cnt - 1, cv, T);
+    } else if ((cnt & 1) && static_cast<uint32_t>(ls) == half) {
+      get(src, 0, sbase + cnt - 1, cv, T);
       put(dst, 0, lane, cv, T);
     }
     __syncthreads();
     cur ^= 1;
     cnt = half + (cnt & 1);
   }
-  if (lane == 0) {
+  if (ls == 0 && live) {
     uint32_t r[8];
     const uint32_t *src = nodes + cur * 8 * T;
-    get(src, 0, 0, left, T);
-    get(src, 0, 1, r, T);
+    get(src, 0, sbase, left, T);
+    get(src, 0, sbase + 1, r, T);
     parent_dev(cv, left, r, b3::kRoot);
     store_hash(o, cv);
   }
@@ -273,16 +286,25 @@ hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
   if (count == 0) return hipSuccess;
   if (len > kB3MaxLen) return hipErrorInvalidValue;
   const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
-  // Threads per shard: enough lanes that each owns >= 2 chunks (pairs are
-  // hashed interleaved), between one and four waves.
-  int T = kB3Threads;
-  while (T > 64 && static_cast<uint64_t>(T) * 2 > n) T >>= 1;
+  // Lanes per shard L: enough that each owns >= 2 chunks (pairs hash
+  // interleaved), a power of two; L >= 64 takes a workgroup of L (at most
+  // 256) lanes per shard, smaller L packs 256 / L shards into a workgroup
+  // (a 16 KiB shard used to leave 3/4 of its wave idle).
+  // (n >= 2 needs L >= 2: the root is the parent of the segment's first two
+  // group nodes, so a segment must end with at least two of them.)
+  uint32_t L = n >= 2 ? 2 : 1;
+  while (L < kB3Threads && static_cast<uint64_t>(L) * 2 < n) L <<= 1;
+  const int T = L >= 64 ? static_cast<int>(L) : kB3Threads;
+  uint32_t seg_log2 = 0;
+  while ((1u << seg_log2) < L) seg_log2++;
   uint32_t q_log2 = 0;
-  while ((static_cast<uint64_t>(T) << q_log2) < n) q_log2++;
+  while ((static_cast<uint64_t>(L) << q_log2) < n) q_log2++;
   const uint32_t depth = q_log2 + 1;
-  const size_t lds = (static_cast<size_t>(depth) + 2) * 8 * T * sizeof(uint32_t);
-  hipLaunchKernelGGL(blake3_batch_kernel, dim3(count), dim3(T), lds, s, in, len, stride, out,
-                     q_log2, depth);
+  const size_t lds = n == 1 ? 0 : (static_cast<size_t>(depth) + 2) * 8 * T * sizeof(uint32_t);
+  const uint32_t per_block = static_cast<uint32_t>(T) / L;
+  const uint32_t blocks = (count + per_block - 1) / per_block;
+  hipLaunchKernelGGL(blake3_batch_kernel, dim3(blocks), dim3(T), lds, s, in, len, stride, out,
+                     count, q_log2, depth, seg_log2);
   return hipGetLastError();
 }
 

@@ -56,7 +56,12 @@ def test_host_hasher_random_sizes():
     (0, 3, 16, 0), (1, 5, 16, 0), (64, 4, 64, 0), (1000, 3, 1024, 0), (1024, 4, 1024, 0),
     (1025, 3, 1040, 0), (4099, 3, 4112, 3), (256 << 10, 6, 256 << 10, 0),
     (300 * 1024 + 5, 2, 300 * 1024 + 16, 0), (1 << 20, 3, 1 << 20, 0),
-    ((1 << 20) + 17, 2, (1 << 20) + 32, 1), (4 << 20, 2, 4 << 20, 0), (16 << 20, 1, 16 << 20, 0)])
+    ((1 << 20) + 17, 2, (1 << 20) + 32, 1), (4 << 20, 2, 4 << 20, 0), (16 << 20, 1, 16 << 20, 0),
+    # several shards per workgroup (segments of 1..32 lanes), counts that
+    # leave the last workgroup partly empty
+    (100, 1000, 112, 0), (2048, 300, 2048, 0), (3 * 1024 + 1, 257, 4096, 0),
+    (16 << 10, 77, 16 << 10, 0), (64 << 10, 33, 64 << 10, 0), (5 * 1024, 9, 5 * 1024 + 16, 3),
+    (127 * 1024, 5, 127 * 1024, 0)])
 def test_device_batch_matches_host(ctx, length, count, stride, offset):
     import torch
     host = np.frombuffer(np.random.default_rng(length + count).bytes(count * stride + offset + 16),
