@@ -302,6 +302,87 @@ def repair_rate(ctx, w, stream, reps=5):
     return res
 
 
+def _time_launches(stream, go, reps):
+    go()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        go()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def config3_assembly(ctx, w, stream, reps=5):
+    """SURVEY 8(d) config 3, "full-chunk assembly reported separately", and
+    its control erasure {9, 10, 11} (parity only: the first 8 survivors are
+    the data shares, decode is pure assembly). decode_chunk returns a fresh
+    chunk (piece.rs:363-387), so here the decode writes a separate chunk
+    buffer: every data share, present or rebuilt, is written once. Fused =
+    the decode kernel stores the present shares from its own loads (one
+    pass: k*B read + k*B written); copy_first = STORB_RS_FUSED_ASSEMBLY=0,
+    survivors copied with hipMemcpy2DAsync before the kernel rebuilds the
+    missing ones (re-reads the k - e present shares)."""
+    k, n, B, N = w.k, w.n, w.B, w.N
+    out = torch.empty_like(w.data)
+    sp = stream.cuda_stream
+    res = {}
+    for erased in ([0, 3, 5], [9, 10, 11]):
+        surv = [i for i in range(n) if i not in erased][:k]
+        row = {"erased": erased, "survivors": surv}
+        for mode in ("fused", "copy_first"):
+            os.environ["STORB_RS_FUSED_ASSEMBLY"] = "1" if mode == "fused" else "0"
+
+            def go():
+                ctx.decode_batch_dev(k, n, B, N, surv, w.dptr, w.pptr, out.data_ptr(),
+                                     stream=sp)
+
+            try:
+                ms = _time_launches(stream, go, reps)
+            finally:
+                os.environ.pop("STORB_RS_FUSED_ASSEMBLY", None)
+            if not torch.equal(out, w.data):
+                raise SystemExit(f"config 3 assembly ({mode}, erased {erased}) mismatch")
+            with torch.cuda.stream(stream):
+                out.zero_()
+            gbs = N * 2 * k * B / (ms * 1e-3) / 1e9
+            row[mode] = {"ms": round(ms, 4),
+                         "GiBps_user": round(N * k * B / GIB / (ms * 1e-3), 1),
+                         "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        res["control" if erased[0] >= k else "erased_data"] = row
+    res["what"] = ("decode into a separate chunk buffer (decode_chunk semantics); bytes = "
+                   "k*B read + k*B written per chunk; fused = assembly inside the decode "
+                   "kernel, copy_first = survivors copied before the kernel")
+    return res
+
+
+def config4_storb_faithful(ctx, w, stream, reps=5):
+    """SURVEY 8(d) config 4 secondary figure: Storb's own sizing of a 1 MiB
+    object (upload.rs:209 piece_length(1 MiB) = 256 KiB chunks; piece.rs:307-317
+    get_k_and_m(256 KiB) = (2, 3)): 4 chunks of 256 KiB per object, each k=2,
+    m=3 (B = 128 KiB). The rank's objects are contiguous, so its chunks are
+    too: one batched launch over 4*N stripes."""
+    from storb_amd import piece as P
+    plen = P.piece_length(w.chunk)
+    k, n = P.get_k_and_m(plen)
+    B = -(-plen // k)
+    stripes = w.N * (w.chunk // plen)
+    par = torch.empty(stripes * (n - k) * B, dtype=torch.uint8, device=w.data.device)
+    sp = stream.cuda_stream
+
+    def go():
+        ctx.encode_batch_dev(k, n, B, stripes, w.dptr, par.data_ptr(), stream=sp)
+
+    ms = _time_launches(stream, go, reps)
+    gbs = stripes * n * B / (ms * 1e-3) / 1e9
+    return {"chunk_bytes": plen, "k": k, "m_total": n, "shard_bytes": B, "stripes": stripes,
+            "ms": round(ms, 4), "GiBps_user": round(w.N * w.chunk / GIB / (ms * 1e-3), 1),
+            "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "kernel": f"rs_apply_perm<{k},{n - k}>",
+            "what": "Storb-faithful sizing of the same objects: 1 MiB object -> 4 x 256 KiB "
+                    "chunks, k=2, m=3, one batched launch; bytes = k*B read + (n-k)*B written"}
+
+
 def kernel_names(kernel, w):
     """The kernels the legs launch (rs_bitslice.hpp / rs_device.hpp)."""
     names = {}
@@ -545,6 +626,10 @@ def main():
         if a.config in (2, 5):
             out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
             out["repair"] = repair_rate(ctx, w, stream)
+        if a.config == 3:
+            out["assembly"] = config3_assembly(ctx, w, stream)
+        if a.config == 4:
+            out["storb_faithful"] = config4_storb_faithful(ctx, w, stream)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

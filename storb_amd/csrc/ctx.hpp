@@ -148,9 +148,15 @@ Variant pick_variant(const storb_rs_ctx *ctx);
 int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
                hipStream_t s, const Tables **out);
 // out_r = sum_j coef[r][j] * in_j for every stripe, tiled onto kernel slots.
+// copy[j] != null (fused assembly, copy_fusable() true): input j is also
+// stored to copy[j] as the kernel reads it; rows may then be 0.
 int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
           const uint8_t *const *d_in, const size_t *in_stride, uint8_t *const *d_out,
-          const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s);
+          const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s,
+          uint8_t *const *copy = nullptr, const size_t *copy_stride = nullptr);
+bool copy_fusable(const storb_rs_ctx *ctx, uint32_t k, size_t block,
+                  const uint8_t *const *d_in, const size_t *in_stride, size_t out_stride,
+                  const uint8_t *d_out);
 // Parity rows of (k, n): the bit-sliced encoder where compiled in, else apply.
 int encode_apply(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *d_in,
                  const size_t *in_stride, uint8_t *const *d_out, const size_t *out_stride,

@@ -125,7 +125,30 @@ __device__ __forceinline__ void load_group(const ApplyArgs &a, uint32_t k, uint3
 // VGPRs and scratch spills at k = 8, r = 4). Per input the selectors are
 // computed once; per (row, input) the table is read from SGPRs right
 // before its v_perm_b32s, and a sched_barrier stops the hoisting.
-template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD>
+// Fused assembly (COPY): a decode into a separate chunk buffer stores each
+// surviving data share straight from the registers it was loaded into, so
+// the chunk is assembled in the same pass (k*B read + k*B written instead of
+// a separate copy pass re-reading the k - e present shares).
+template <int G, int T, int U, bool GUARD>
+__device__ __forceinline__ void copy_group(const ApplyArgs &a, uint32_t k, uint32_t cols,
+                                           uint32_t stripe, uint32_t c0, int g,
+                                           const u32x4 (&src)[G][U]) {
+#pragma unroll
+  for (int jj = 0; jj < G; jj++) {
+    const int j = g * G + jj;
+    if (j >= static_cast<int>(k) || a.copy[j] == nullptr) continue;
+    u32x4 *q = reinterpret_cast<u32x4 *>(a.copy[j] + static_cast<uint64_t>(stripe) *
+                                                         a.copy_stride[j]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t c = c0 + u * T;
+      if (!GUARD || c < cols) st_stream(q + c, src[jj][u]);
+    }
+  }
+}
+
+template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD,
+          bool COPY = false>
 __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tabs,
                                           uint32_t k, uint32_t r, uint32_t cols,
                                           uint32_t stripe, uint32_t c0) {
@@ -142,6 +165,10 @@ __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tab
   for (int g = 0; g < NG; g++) {
     if (g + 1 < NG)
       load_group<KM, G, T, U, GUARD>(a, k, cols, stripe, c0, g + 1, buf[(g + 1) & 1]);
+    if constexpr (COPY) {
+      copy_group<G, T, U, GUARD>(a, k, cols, stripe, c0, g, buf[g & 1]);
+      if (r == 0) continue;  // pure assembly: nothing missing
+    }
     if constexpr (PAIR) {
       // Inputs two at a time: per (row, dword) the six v_perm_b32 lookups
       // of inputs j and j+1 fold into acc with three 3-input XORs (instead
@@ -239,7 +266,8 @@ __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tab
 // scalar branches; they also split the body into basic blocks, which keeps
 // the scheduler from hoisting every table load and selector (a guard-free
 // "exact" specialisation measured 181-256 VGPRs and scratch spills).
-template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false,
+          bool COPY = false>
 __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
   constexpr uint32_t TILE = T * U;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
@@ -249,18 +277,18 @@ __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
   const PermTab *tabs = a.ptab;
   if constexpr (TL) {
     __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * RM];
-    const uint32_t n16 = a.k * RM * (sizeof(PermTab) / 16);
+    const uint32_t n16 = (COPY && a.r == 0) ? 0u : a.k * RM * (sizeof(PermTab) / 16);
     for (uint32_t t = threadIdx.x; t < n16; t += T)
       reinterpret_cast<u32x4 *>(lds_ptab)[t] = reinterpret_cast<const u32x4 *>(a.ptab)[t];
     __syncthreads();
     tabs = lds_ptab;
   }
   if (base + TILE <= cols)
-    perm_tile<KM, RM, T, U, BAR, G, PAIR, false>(a, tabs, a.k, a.r, cols, stripe,
-                                               base + threadIdx.x);
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(a, tabs, a.k, a.r, cols, stripe,
+                                                      base + threadIdx.x);
   else
-    perm_tile<KM, RM, T, U, BAR, G, PAIR, true>(a, tabs, a.k, a.r, cols, stripe,
-                                              base + threadIdx.x);
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(a, tabs, a.k, a.r, cols, stripe,
+                                                     base + threadIdx.x);
 }
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
@@ -269,8 +297,16 @@ hipError_t launch_perm(const ApplyArgs &a, hipStream_t s) {
   const uint64_t blocks = ((cols + T * U - 1) / (T * U)) * a.nstripes;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR>), dim3(blocks), dim3(T), 0,
-                     s, a);
+  if (a.ncopy) {
+    if constexpr (KM <= static_cast<int>(kCopyMaxK))
+      hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR, true>), dim3(blocks),
+                         dim3(T), 0, s, a);
+    else
+      return hipErrorInvalidValue;
+  } else {
+    hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR>), dim3(blocks), dim3(T),
+                       0, s, a);
+  }
   return hipGetLastError();
 }
 
@@ -366,6 +402,7 @@ hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
 template <int KM>
 hipError_t go_perm_r(const ApplyArgs &a, hipStream_t s) {
   switch (rows_bucket(a.r)) {
+    case 0:  // pure assembly (COPY with nothing missing); tables of one zero row
     case 1: return go_perm<KM, 1>(a, s);
     case 2: return go_perm<KM, 2>(a, s);
     case 3: return go_perm<KM, 3>(a, s);

@@ -71,6 +71,8 @@ __global__ __launch_bounds__(kThreads) void fill_splitmix_kernel(
 
 bool vector_ok(const ApplyArgs &a) {
   if (a.block % 16) return false;
+  for (uint32_t j = 0; a.ncopy && j < a.k; j++)
+    if ((reinterpret_cast<uintptr_t>(a.copy[j]) | a.copy_stride[j]) % 16) return false;
   for (uint32_t j = 0; j < a.k; j++)
     if ((reinterpret_cast<uintptr_t>(a.in[j]) | a.in_stride[j]) % 16) return false;
   for (uint32_t i = 0; i < a.r; i++)
@@ -79,9 +81,14 @@ bool vector_ok(const ApplyArgs &a) {
 }
 
 hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s) {
-  if (a.k == 0 || a.r == 0 || a.k > kSlotK || a.r > kSlotR ||
-      a.tab_rows != static_cast<uint32_t>(rows_bucket(a.r)))
+  if (a.k == 0 || a.k > kSlotK || a.r > kSlotR ||
+      a.tab_rows != static_cast<uint32_t>(rows_bucket(a.r ? a.r : 1)))
     return hipErrorInvalidValue;
+  // Fused assembly runs only in the dwordx4 register-table kernels; the host
+  // (copy_fusable) checks that before asking for it.
+  if (a.ncopy && (a.k > kCopyMaxK || v != Variant::Perm || !vector_ok(a)))
+    return hipErrorInvalidValue;
+  if (a.r == 0 && !a.ncopy) return hipErrorInvalidValue;
   if (a.block == 0 || a.nstripes == 0) return hipSuccess;
   if (!vector_ok(a)) {
     const uint64_t words = (a.block + 3) >> 2;

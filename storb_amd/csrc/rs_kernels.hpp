@@ -34,7 +34,17 @@ struct ApplyArgs {
   uint64_t block;       // bytes per share
   uint32_t nstripes;
   uint32_t accumulate;  // 1: out ^= result (column tiling), 0: out = result
+  // Fused assembly (decode into a separate chunk buffer): input slot j is
+  // also stored, as loaded, to copy[j] (null = not copied). ncopy > 0 selects
+  // the COPY kernels (KM <= kCopyMaxK); r may then be 0 (pure assembly).
+  uint32_t ncopy;
+  uint8_t *copy[kSlotK];
+  uint64_t copy_stride[kSlotK];
 };
+
+// Largest k bucket with COPY instantiations; wider decodes copy survivors
+// with hipMemcpy2DAsync before the kernel.
+constexpr uint32_t kCopyMaxK = 16;
 
 enum class Variant { Perm = 1, Lds = 2 };
 

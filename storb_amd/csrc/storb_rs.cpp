@@ -124,29 +124,39 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
 }
 
 // out_r = sum_j coef[r][j] * in_j for all stripes, tiled into slot blocks.
+// copy (optional, fused assembly): copy[j] != null stores input j there as
+// it is loaded (copy_fusable() must hold); rows may then be 0.
 int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
           const uint8_t *const *d_in, const size_t *in_stride, uint8_t *const *d_out,
-          const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s) {
-  if (rows == 0 || block == 0 || nstripes == 0) return STORB_RS_OK;
+          const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s,
+          uint8_t *const *copy, const size_t *copy_stride) {
+  if ((rows == 0 && !copy) || block == 0 || nstripes == 0) return STORB_RS_OK;
   const Tables *t = nullptr;
-  int rc = get_tables(ctx, k, rows, coef, s, &t);
+  const std::vector<uint8_t> zero_row(k, 0);
+  const uint32_t trows = rows ? rows : 1;  // pure assembly: one zero row of tables
+  int rc = get_tables(ctx, k, trows, rows ? coef : zero_row.data(), s, &t);
   if (rc) return rc;
   const Variant v = pick_variant(ctx);
   size_t bi = 0;
-  for (uint32_t rb = 0; rb < rows; rb += kSlotR)
+  for (uint32_t rb = 0; rb < trows; rb += kSlotR)
     for (uint32_t cb = 0; cb < k; cb += kSlotK, bi++) {
       ApplyArgs a{};
-      a.r = std::min<uint32_t>(kSlotR, rows - rb);
+      a.r = std::min<uint32_t>(kSlotR, rows - std::min(rows, rb));
       a.k = std::min<uint32_t>(kSlotK, k - cb);
       for (uint32_t j = 0; j < a.k; j++) {
         a.in[j] = d_in[cb + j];
         a.in_stride[j] = in_stride[cb + j];
+        if (copy && rb == 0 && copy[cb + j]) {  // each input copied once
+          a.copy[j] = copy[cb + j];
+          a.copy_stride[j] = copy_stride[cb + j];
+          a.ncopy++;
+        }
       }
       for (uint32_t i = 0; i < a.r; i++) {
         a.out[i] = d_out[rb + i];
         a.out_stride[i] = out_stride[rb + i];
       }
-      a.tab_rows = static_cast<uint32_t>(rows_bucket(a.r));
+      a.tab_rows = static_cast<uint32_t>(rows_bucket(a.r ? a.r : 1));
       a.ptab = reinterpret_cast<const PermTab *>(t->dev) + t->b_off[bi];
       a.btab = t->dev + t->perm_bytes + t->b_off[bi] * 256;
       a.block = block;
@@ -155,6 +165,23 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
       HIP_TRY(ctx, launch_apply(a, v, s));
     }
   return STORB_RS_OK;
+}
+
+// Whether a decode into a separate buffer can assemble the chunk inside the
+// kernel: the COPY instantiations exist for k <= kCopyMaxK in the dwordx4
+// register-table kernel (not the LDS comparison variant), and every share
+// base / stride must be 16-B aligned.
+bool copy_fusable(const storb_rs_ctx *ctx, uint32_t k, size_t block,
+                  const uint8_t *const *d_in, const size_t *in_stride, size_t out_stride,
+                  const uint8_t *d_out) {
+  if (k > kCopyMaxK || pick_variant(ctx) != Variant::Perm || block % 16 ||
+      out_stride % 16 || reinterpret_cast<uintptr_t>(d_out) % 16)
+    return false;
+  for (uint32_t j = 0; j < k; j++)
+    if ((reinterpret_cast<uintptr_t>(d_in[j]) | in_stride[j]) % 16) return false;
+  // STORB_RS_FUSED_ASSEMBLY=0: copy first (kept for the A/B measurement)
+  return std::getenv("STORB_RS_FUSED_ASSEMBLY") == nullptr ||
+         std::getenv("STORB_RS_FUSED_ASSEMBLY")[0] != '0';
 }
 
 // Parity of (k, n) = enc[k..n) * data. Under the AUTO variant the geometries
@@ -563,19 +590,27 @@ int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t 
       ins[c] = parity_stride;
     }
   }
-  // Surviving data shares: in place when d_out aliases d_data, else copied.
-  if (d_out != d_data || out_stride != data_stride) {
-    for (uint32_t c = 0; c < k; c++)
-      if (slot_idx[c] < k)
-        HIP_TRY(ctx, hipMemcpy2DAsync(d_out + static_cast<size_t>(c) * block, out_stride,
-                                      in[c], ins[c], block, nstripes,
-                                      hipMemcpyDeviceToDevice, s));
-  }
-  if (missing.empty()) return STORB_RS_OK;
   std::vector<uint8_t *> out(missing.size());
   std::vector<size_t> outs(missing.size(), out_stride);
   for (size_t r = 0; r < missing.size(); r++)
     out[r] = d_out + static_cast<size_t>(missing[r]) * block;
+  // Surviving data shares: in place when d_out aliases d_data; else stored
+  // to their slots of d_out by the decode kernel itself as it reads them
+  // (fused assembly), or, where that kernel does not apply, copied first.
+  if (d_out != d_data || out_stride != data_stride) {
+    std::vector<uint8_t *> copy(k, nullptr);
+    std::vector<size_t> copys(k, out_stride);
+    for (uint32_t c = 0; c < k; c++)
+      if (slot_idx[c] < k) copy[c] = d_out + static_cast<size_t>(c) * block;
+    if (copy_fusable(ctx, k, block, in.data(), ins.data(), out_stride, d_out))
+      return apply(ctx, k, static_cast<uint32_t>(missing.size()), coef.data(), in.data(),
+                   ins.data(), out.data(), outs.data(), block, nstripes, s, copy.data(),
+                   copys.data());
+    for (uint32_t c = 0; c < k; c++)
+      if (copy[c])
+        HIP_TRY(ctx, hipMemcpy2DAsync(copy[c], out_stride, in[c], ins[c], block, nstripes,
+                                      hipMemcpyDeviceToDevice, s));
+  }
   return apply(ctx, k, static_cast<uint32_t>(missing.size()), coef.data(), in.data(),
                ins.data(), out.data(), outs.data(), block, nstripes, s);
 }

@@ -328,6 +328,49 @@ def test_dev_decode_roundtrip(ctx, k, n, erased, inplace):
     assert np.array_equal(out.cpu().numpy(), host)
 
 
+FUSED_CASES = [(4, 6, (0, 1)), (4, 6, ()), (4, 6, (4, 5)), (8, 12, (0, 3, 5)),
+               (8, 12, (9, 10, 11)), (16, 24, (0, 1)), (16, 24, tuple(range(0, 16, 2))),
+               (3, 5, (2,)), (12, 18, (11,)), (2, 3, (1,))]
+
+
+@pytest.mark.parametrize("k,n,erased", FUSED_CASES)
+@pytest.mark.parametrize("B,ns", [(4096 * 2, 5), (4096 * 3 + 16 * 5, 3)])
+@pytest.mark.parametrize("mode", ["fused", "copy_first", "lds", "strided"])
+def test_dev_decode_separate_output_assembly(ctx, monkeypatch, k, n, erased, B, ns, mode):
+    """decode_chunk returns a fresh chunk (piece.rs:363-387): decode into a
+    separate buffer stores every surviving data share from the decode
+    kernel's own loads (fused assembly, k <= 16) -- full tiles and a ragged
+    last tile, nothing missing (pure assembly) and a strided output --
+    byte-identical to copying the survivors first (STORB_RS_FUSED_ASSEMBLY=0)
+    and to the LDS comparison variant, and every stripe equals the input."""
+    host = rnd(ns * k * B, 7 * k + n + B + len(erased))
+    data = to_dev(host)
+    par = torch.zeros(ns * (n - k) * B, dtype=torch.uint8, device=DEV)
+    ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
+    survivors = [i for i in range(n) if i not in erased]
+    random.Random(B + k).shuffle(survivors)
+    view = data.view(ns, k, B)
+    for e in erased:
+        if e < k:
+            view[:, e].fill_(0xA5)
+    pad = 3 * 16 if mode == "strided" else 0
+    ostride = k * B + pad
+    out = torch.full((ns * ostride,), 0x5A, dtype=torch.uint8, device=DEV)
+    if mode == "copy_first":
+        monkeypatch.setenv("STORB_RS_FUSED_ASSEMBLY", "0")
+    if mode == "lds":
+        ctx.set_kernel(_lib.KERNEL_LDS)
+    try:
+        ctx.decode_batch_dev(k, n, B, ns, survivors, data.data_ptr(), par.data_ptr(),
+                             out.data_ptr(), out_stride=ostride if pad else 0)
+        ctx.sync()
+    finally:
+        ctx.set_kernel(_lib.KERNEL_AUTO)
+    got = out.cpu().numpy().reshape(ns, ostride)
+    assert np.array_equal(got[:, :k * B].reshape(-1), host)
+    assert (got[:, k * B:] == 0x5A).all()  # the stride gap is never written
+
+
 def test_dev_decode_not_enough(ctx):
     d = torch.zeros(4 * 64, dtype=torch.uint8, device=DEV)
     p = torch.zeros(2 * 64, dtype=torch.uint8, device=DEV)
