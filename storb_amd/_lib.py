@@ -169,6 +169,8 @@ def blake3(data) -> bytes:
 def _as_u8(data) -> np.ndarray:
     if isinstance(data, np.ndarray):
         return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    if isinstance(data, memoryview) and data.contiguous:
+        return np.frombuffer(data.cast("B"), dtype=np.uint8)  # zero-copy view
     return np.frombuffer(bytes(data), dtype=np.uint8)
 
 

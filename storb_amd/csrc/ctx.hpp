@@ -141,6 +141,8 @@ inline int hip_fail(storb_rs_ctx *ctx, hipError_t e, const char *what) {
 const std::vector<uint8_t> &cached_enc(uint32_t k, uint32_t n);
 // Contexts created with device -1 take devices round-robin.
 int next_round_robin();
+// Host BLAKE3 hash of len bytes (blake3_host.cpp).
+void blake3_host(const uint8_t *data, size_t len, uint8_t out[32]);
 // [p, p+len) inside one storb_rs_host_alloc / _register range.
 bool range_pinned(const void *p, size_t len);
 Variant pick_variant(const storb_rs_ctx *ctx);

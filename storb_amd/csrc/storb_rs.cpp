@@ -659,40 +659,10 @@ int storb_rs_repair_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t 
                block, nstripes, pick_stream(ctx, hip_stream));
 }
 
-// Host BLAKE3: chunks in order with a stack of complete subtrees; the last
-// chunk is folded right to left so the final parent carries ROOT.
+// Host BLAKE3 (blake3_host.cpp: 16 chunks per AVX-512 compression where
+// the CPU has it, else the scalar compression of blake3.hpp).
 void storb_blake3(const uint8_t *data, size_t len, uint8_t out[32]) {
-  const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
-  uint32_t cv[8];
-  auto emit = [&](const uint32_t *w) {
-    for (int i = 0; i < 8; i++)
-      for (int b = 0; b < 4; b++) out[4 * i + b] = static_cast<uint8_t>(w[i] >> (8 * b));
-  };
-  if (n == 1) {
-    b3::chunk_cv(cv, data, static_cast<uint32_t>(len), 0, b3::kRoot);
-    emit(cv);
-    return;
-  }
-  std::vector<std::array<uint32_t, 8>> stack;
-  for (uint64_t c = 0; c + 1 < n; c++) {
-    b3::chunk_cv(cv, data + c * b3::kChunkLen, b3::kChunkLen, c, 0);
-    for (uint64_t t = c + 1; (t & 1) == 0; t >>= 1) {
-      b3::parent_cv(cv, stack.back().data(), cv, 0);
-      stack.pop_back();
-    }
-    std::array<uint32_t, 8> a;
-    std::memcpy(a.data(), cv, 32);
-    stack.push_back(a);
-  }
-  const uint64_t last = n - 1;
-  b3::chunk_cv(cv, data + last * b3::kChunkLen,
-               static_cast<uint32_t>(len - last * b3::kChunkLen), last, 0);
-  while (!stack.empty()) {
-    const std::array<uint32_t, 8> l = stack.back();
-    stack.pop_back();
-    b3::parent_cv(cv, l.data(), cv, stack.empty() ? b3::kRoot : 0);
-  }
-  emit(cv);
+  blake3_host(data, len, out);
 }
 
 int storb_rs_blake3_batch_dev(storb_rs_ctx *ctx, const uint8_t *d_in, size_t len,

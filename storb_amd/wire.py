@@ -70,13 +70,16 @@ def serialise_piece_response(piece_hash: bytes, data: bytes) -> bytes:
     return piece_hash + struct.pack("<Q", len(data)) + data
 
 
-def deserialise_piece_response(buf: bytes, piece_hash: bytes) -> bytes:
+def deserialise_piece_response(buf, piece_hash: bytes) -> memoryview:
     """piece.rs:238-255 + download.rs:121-164: locate the hash, decode the
-    Vec<u8>, reject trailing bytes, and check blake3(data) == piece_hash."""
-    pos = buf.find(piece_hash)
+    Vec<u8>, reject trailing bytes, and check blake3(data) == piece_hash.
+    Returns a zero-copy view of the piece inside `buf` (no slice copies:
+    fetch threads hold the GIL for every copy of a shard)."""
+    mv = memoryview(buf).cast("B")
+    pos = 0 if bytes(mv[:HASH_LEN]) == piece_hash else bytes(buf).find(piece_hash)
     if pos < 0:
         raise ValueError("piece hash not found in response")
-    rest = buf[pos + HASH_LEN:]
+    rest = mv[pos + HASH_LEN:]
     if len(rest) < 8:
         raise ValueError("truncated response")
     (n,) = struct.unpack("<Q", rest[:8])

@@ -42,6 +42,36 @@ def test_host_hasher_matches_reference(n):
     assert _lib.blake3(tv(n)) == ref(tv(n))
 
 
+@pytest.mark.parametrize("n", [16 * 1024 + 1, 17 * 1024, 33 * 1024, 33 * 1024 + 1, 65 * 1024,
+                               (256 << 10) + 1, (512 << 10) + 1024, (1 << 20) + 1])
+def test_host_hasher_simd_subtrees(n):
+    """Sizes whose first n-1 chunks decompose into subtrees of >= 16 chunks:
+    the AVX-512 path (16 chunks and 16 parents per compression) where the
+    CPU has it, against the restated reference."""
+    d = random.Random(n).randbytes(n)
+    assert _lib.blake3(d) == ref(d)
+
+
+def test_host_hasher_simd_equals_scalar_large():
+    """Up to 9 MiB (Storb's 8 MiB shard sizing and beyond): the SIMD hasher
+    against the scalar compression of the same library (STORB_B3_SCALAR=1 in
+    a child process), which the tests above pin to the reference."""
+    import subprocess
+    import sys
+    sizes = [(8 << 20), (8 << 20) + 3, (9 << 20) - 1024 * 17 + 5, (2 << 20) + 1024 * 31]
+    rng = np.random.default_rng(11)
+    data = [rng.bytes(n) for n in sizes]
+    mine = [_lib.blake3(d).hex() for d in data]
+    code = ("import sys, numpy as np; from storb_amd import _lib; "
+            "rng = np.random.default_rng(11); "
+            f"print(' '.join(_lib.blake3(rng.bytes(n)).hex() for n in {sizes}))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, STORB_B3_SCALAR="1")
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, check=True,
+                         capture_output=True, text=True).stdout.split()
+    assert out == mine
+
+
 def test_host_hasher_random_sizes():
     rng = random.Random(3)
     for _ in range(12):
