@@ -91,6 +91,16 @@ def test_miner_store_and_retrieve(tmp_path):
         c = http.client.HTTPConnection("127.0.0.1", hp, timeout=10)
         c.request("GET", f"/piece?piecehash={'00' * 32}&handshake=00")
         assert c.getresponse().status == 500
+        # the harness's keep-alive client: every piece over one connection,
+        # then a missing one, then a good one again on the same connection
+        pc = wire.PieceClient("127.0.0.1", hp)
+        for p, h in list(zip(pieces, acks)) * 2:
+            st, body = pc.get(h.hex(), bytes(96).hex())
+            assert st == 200 and wire.deserialise_piece_response(body, h) == p
+        assert pc.get("00" * 32, "00")[0] == 500
+        st, body = pc.get(acks[0].hex(), "00")
+        assert st == 200 and wire.deserialise_piece_response(body, acks[0]) == pieces[0]
+        pc.close()
     finally:
         proc.kill()
         proc.wait()

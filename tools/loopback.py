@@ -20,7 +20,6 @@ usage: python tools/loopback.py [--size BYTES] [--miners N]   (prints one JSON l
 from __future__ import annotations
 
 import argparse
-import http.client
 import http.server
 import json
 import os
@@ -74,15 +73,17 @@ def miner_main(a):
                 if u.path != "/piece" or "handshake" not in q:
                     raise ValueError
                 hexhash = q["piecehash"][0]
-                body = wire.serialise_piece_response(bytes.fromhex(hexhash),
-                                                     store.read(hexhash))
-                code = 200
-            except Exception:
-                body, code = b"error", 500
-            self.send_response(code)
-            self.send_header("Content-Length", str(len(body)))
-            self.end_headers()
-            self.wfile.write(body)
+                if len(bytes.fromhex(hexhash)) != wire.HASH_LEN:
+                    raise ValueError
+                # routes.rs:188-206: bincode PieceResponse, piece bytes by sendfile
+                store.send_piece_response(self.connection, hexhash,
+                                          b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n")
+            except (OSError, ValueError, KeyError):
+                body = b"error"
+                self.send_response(500)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
 
         def log_message(self, *args):
             pass
@@ -199,11 +200,9 @@ def _run(a, miners):
             conns = tls.conns = {}
         c = conns.get(m)
         if c is None:
-            c = conns[m] = http.client.HTTPConnection("127.0.0.1", miners[m]["http"], timeout=10)
-        c.request("GET", f"/piece?piecehash={hexhash}&handshake={HANDSHAKE.hex()}")
-        r = c.getresponse()
-        body = r.read()
-        if r.status != 200:
+            c = conns[m] = wire.PieceClient("127.0.0.1", miners[m]["http"])
+        status, body = c.get(hexhash, HANDSHAKE.hex())
+        if status != 200:
             raise IOError("miner error")
         return body
 
@@ -217,9 +216,11 @@ def _run(a, miners):
             try:
                 body = fetch(meta["miner"][i], h.hex())
                 got[i] = wire.deserialise_piece_response(body, h)  # blake3 check
-            except (OSError, ValueError, http.client.HTTPException):
+            except (OSError, ValueError):
                 if hasattr(tls, "conns"):
-                    tls.conns.pop(meta["miner"][i], None)
+                    c = tls.conns.pop(meta["miner"][i], None)
+                    if c is not None:
+                        c.close()
         return ci, got
 
     with ThreadPoolExecutor(16) as ex:
