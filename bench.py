@@ -51,8 +51,8 @@ SEED_BASE = 0x5709B
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                    help="BASELINE config; 5 = the device-resident GPU half of config 5 "
                         "(1 GiB object -> 128 x 8 MiB chunks, storb k=16, m=24)")
@@ -65,6 +65,10 @@ def parse():
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--leg-events", choices=["each", "ends"], default="ends",
+                   help="ends: HIP events only around the timed region, per-leg times "
+                        "from a separate untimed pass; each: an event after every leg "
+                        "inside the timed region (costs 2.5-3 %% of the step)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal of the "
                         "multi-rank logic with several ranks on one GPU, see "
@@ -530,23 +534,47 @@ def main():
             f()
     stream.synchronize()
 
+    # Timed region: K steps with one HIP event at each end on the launch
+    # stream (a timing event after every leg costs 2.5-3 % of the step:
+    # profiles/r1_leg_events.txt). GPU time per step = region / K.
+    e_start = torch.cuda.Event(enable_timing=True)
+    e_end = torch.cuda.Event(enable_timing=True)
+    each = a.leg_events == "each"
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(legs) + 1)]
-          for _ in range(a.steps)]
+          for _ in range(a.steps if each else 0)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e_start.record(stream)
     for i in range(a.steps):
-        ev[i][0].record(stream)
+        if each:
+            ev[i][0].record(stream)
         for j, f in enumerate(legs):
             f()
-            ev[i][j + 1].record(stream)
+            if each:
+                ev[i][j + 1].record(stream)
+    e_end.record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    leg_ms = [sum(e[j].elapsed_time(e[j + 1]) for e in ev) / a.steps for j in range(len(legs))]
+    gpu_ms = e_start.elapsed_time(e_end) / a.steps
+    if not each:
+        # Per-leg split (which kernel took what) from an untimed pass of the
+        # same steps with an event after every leg; reported, not used for
+        # `value` or `achieved`.
+        n_probe = min(a.steps, 50)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(legs) + 1)]
+              for _ in range(n_probe)]
+        for i in range(n_probe):
+            ev[i][0].record(stream)
+            for j, f in enumerate(legs):
+                f()
+                ev[i][j + 1].record(stream)
+        stream.synchronize()
+    leg_ms = [sum(e[j].elapsed_time(e[j + 1]) for e in ev) / len(ev) for j in range(len(legs))]
     units = w.N * w.chunk * len(legs)  # user bytes per step on this rank
     if world > 1:
         tdev = dev if a.dist_backend == "nccl" else torch.device("cpu")
@@ -560,7 +588,10 @@ def main():
         units_all = float(units)
     value = a.steps * units_all / GIB / elapsed
     alg = {leg: w.alg_bytes(leg) for leg in w.legs}
-    achieved = sum(alg.values()) / (sum(leg_ms) * 1e-3) / 1e9
+    # algorithmic bytes of one step / GPU time of one step in the timed region
+    # (config 2: every launch is rs_apply_perm<4,2> with 1.5 GiB, so this is
+    # also bytes per launch / average launch duration)
+    achieved = sum(alg.values()) / (gpu_ms * 1e-3) / 1e9
 
     traffic = None
     tpath = os.path.join(HERE, "profiles", "pmc_traffic.json")
@@ -603,7 +634,11 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "kernel": kernel_names(a.kernel, w),
+            "gpu_ms_per_step": round(gpu_ms, 4),
+            "launch_ms": round(gpu_ms / len(legs), 4),
             "leg_ms": {leg: round(ms, 4) for leg, ms in zip(w.legs, leg_ms)},
+            "leg_ms_source": ("events after every leg inside the timed region" if each else
+                              "separate untimed pass with an event after every leg"),
             "alg_bytes_per_launch": alg,
             "copy_ceiling_gbs": None,
         },

@@ -11,7 +11,7 @@ ROUND=${1:-r1}
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/prof_$ROUND
 rm -rf "$OUT" && mkdir -p "$OUT"
-KSUB="rs_apply_perm<4, 2, 256, 1, false, 4, false, false>"
+KSUB="rs_apply_perm<4, 2, 256, 1, false, 4, false, false, false>"
 # --no-host-path: the PCIe legs launch the same kernel on host-staged batches
 # (18 us .. 3.6 ms each), which would blend into its average; this run's own
 # bench line (bench_traced.log) is the one the stats are compared with.
