@@ -18,9 +18,17 @@ Here the same results come from whole-object calls: every run of chunks of
 one geometry is ONE ``storb_rs_encode_chunks_hashed`` (parity and every
 piece id on the GPU) or ONE ``storb_rs_decode_chunks``. Bytes, hashes and
 metadata rows are identical to the per-chunk path (tests/test_objects.py).
+
+Several GPUs (BASELINE config 5 on 8 x MI355X, SURVEY 8(e): chunks of a single
+huge object partition across the devices of a node): pass ``contexts`` (one
+``Context`` per device, e.g. ``device_contexts()``) and every run is cut into
+one contiguous slice of chunks per context, all slices in flight at once
+(one host thread per context; the calls release the GIL). No data moves
+between devices: each slice is host in / host out on its own GPU.
 """
 from __future__ import annotations
 
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -82,10 +90,42 @@ def _runs(spans: Sequence[Tuple[int, int]]):
         i = j
 
 
-def encode_object(data, ctx: Optional[_lib.Context] = None) -> EncodedObject:
+def device_contexts(ndev: Optional[int] = None) -> List[_lib.Context]:
+    """One context per visible device (the first `ndev` of them)."""
+    n = _lib.device_count() if ndev is None else ndev
+    return [_lib.Context(d % max(_lib.device_count(), 1)) for d in range(n)]
+
+
+def _slices(cnt: int, parts: int) -> List[Tuple[int, int]]:
+    """Split chunks [0, cnt) into <= parts contiguous non-empty ranges."""
+    parts = max(1, min(parts, cnt))
+    q, r = divmod(cnt, parts)
+    out, a = [], 0
+    for i in range(parts):
+        b = a + q + (i < r)
+        out.append((a, b))
+        a = b
+    return out
+
+
+def _fan_out(ctxs, cnt: int, call) -> None:
+    """call(ctx, a, b) for one contiguous slice of [0, cnt) per context, the
+    slices concurrently; the first error is raised."""
+    sl = _slices(cnt, len(ctxs))
+    if len(sl) == 1:
+        call(ctxs[0], *sl[0])
+        return
+    with ThreadPoolExecutor(len(sl)) as ex:
+        for f in [ex.submit(call, c, a, b) for c, (a, b) in zip(ctxs, sl)]:
+            f.result()
+
+
+def encode_object(data, ctx: Optional[_lib.Context] = None,
+                  contexts: Optional[Sequence[_lib.Context]] = None) -> EncodedObject:
     """encode_chunk + piece hashing + ChunkValue / PieceValue for a whole
-    object; one batched GPU call per run of equal-length chunks."""
-    ctx = ctx or _lib.thread_context()
+    object; one batched GPU call per run of equal-length chunks (per
+    context, when `contexts` spreads the run over several GPUs)."""
+    ctxs = list(contexts) if contexts else [ctx or _lib.thread_context()]
     buf = data if isinstance(data, np.ndarray) else np.frombuffer(bytes(data), np.uint8)
     buf = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
     spans = chunk_spans(buf.size)
@@ -97,8 +137,14 @@ def encode_object(data, ctx: Optional[_lib.Context] = None) -> EncodedObject:
         cnt = c1 - c0
         k, m = _lib.get_k_and_m(ln)
         B = _lib.block_size(k, ln)
-        par, ids = ctx.encode_chunks_hashed(k, m, buf[off:off + cnt * ln], ln, cnt)
-        par = par.reshape(cnt, m - k, B)
+        par = np.empty((cnt, m - k, B), np.uint8)
+        ids = np.empty((cnt, m, 32), np.uint8)
+
+        def enc(cx, a, b, off=off, ln=ln, k=k, m=m, par=par, ids=ids):
+            cx.encode_chunks_hashed(k, m, buf[off + a * ln:off + b * ln], ln, b - a,
+                                    out=par[a:b].reshape(-1), hashes=ids[a:b])
+
+        _fan_out(ctxs, cnt, enc)
         for c in range(cnt):
             chunk = buf[off + c * ln:off + (c + 1) * ln]
             if B * k != ln:
@@ -114,13 +160,14 @@ def encode_object(data, ctx: Optional[_lib.Context] = None) -> EncodedObject:
 
 
 def reconstruct_object(chunks: Sequence[ChunkValue], fetched: Sequence[Dict[int, bytes]],
-                       ctx: Optional[_lib.Context] = None) -> np.ndarray:
+                       ctx: Optional[_lib.Context] = None,
+                       contexts: Optional[Sequence[_lib.Context]] = None) -> np.ndarray:
     """The download side: fetched[c] maps piece_idx -> piece bytes of chunk c
     (any subset); each chunk rebuilds from its first k pieces by index
     (reconstruct_chunk); PieceError if a chunk has fewer than k. One batched
     GPU call per run of chunks of one geometry. Returns the object's bytes
     as a uint8 array (no extra copy into a bytes object)."""
-    ctx = ctx or _lib.thread_context()
+    ctxs = list(contexts) if contexts else [ctx or _lib.thread_context()]
     for ci, (cv, got) in enumerate(zip(chunks, fetched)):
         if len(got) < cv.k:
             raise PieceError(ci, cv.k, len(got))
@@ -138,7 +185,12 @@ def reconstruct_object(chunks: Sequence[ChunkValue], fetched: Sequence[Dict[int,
         for c in range(i, j):
             ids = sorted(fetched[c])
             batch.append(([fetched[c][x] for x in ids], ids))
-        ctx.decode_chunks(k, m, B, pad, batch, out=out[off:off + (j - i) * ln].reshape(j - i, ln))
+        dst = out[off:off + (j - i) * ln].reshape(j - i, ln)
+
+        def dec(cx, a, b, k=k, m=m, B=B, pad=pad, batch=batch, dst=dst):
+            cx.decode_chunks(k, m, B, pad, batch[a:b], out=dst[a:b])
+
+        _fan_out(ctxs, j - i, dec)
         off += (j - i) * ln
         i = j
     return out

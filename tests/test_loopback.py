@@ -107,10 +107,14 @@ def test_miner_store_and_retrieve(tmp_path):
 
 
 @pytest.mark.gpu
-def test_loopback_roundtrip_small():
+@pytest.mark.parametrize("gpus", [0, 3])
+def test_loopback_roundtrip_small(gpus):
+    """gpus=3: the chunks partition over three contexts (several per device
+    on a one-GPU box), the config-5 layout for 8 x MI355X."""
     import loopback
     res = loopback.run(argparse.Namespace(size=(24 << 20) + 12345, miners=4, seed=1,
-                                          kill_seed=7))
+                                          kill_seed=7, gpus=gpus))
     assert res["bit_exact"]
     assert res["ack_mismatch"] == 0
     assert res["chunks_decoded_through_parity"] > 0
+    assert res["contexts"] == (gpus or max(1, res["visible_gpus"]))

@@ -90,3 +90,43 @@ def test_reconstruct_object_under_erasures(ctx):
     with pytest.raises(PieceError) as e:
         objects.reconstruct_object(enc.chunks, bad, ctx)
     assert (e.value.chunk_idx, e.value.k, e.value.got) == (1, cv0.k, cv0.k - 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nctx", [2, 3, 5])
+def test_object_calls_partitioned_over_contexts(ctx, nctx):
+    """Chunks of one object spread over several contexts (one per GPU on a
+    node; here several share the one device) give the same shares, piece
+    ids, rows and reconstruction as one context -- including runs shorter
+    than the context count and the short tail chunk."""
+    ctxs = objects.device_contexts(nctx)
+    try:
+        for total in (40 << 20, 9 * (1 << 20) + 7):
+            data = _obj(total, nctx + total % 13)
+            one = objects.encode_object(data, ctx)
+            many = objects.encode_object(data, contexts=ctxs)
+            assert one.chunks == many.chunks and one.pieces == many.pieces
+            for a, b in zip(one.data, many.data):
+                assert all(np.array_equal(np.asarray(x), np.asarray(y)) for x, y in zip(a, b))
+            rng = random.Random(nctx)
+            fetched = []
+            for cv, sh in zip(many.chunks, many.data):
+                keep = rng.sample(range(cv.m), cv.k)
+                fetched.append({i: np.asarray(sh[i]).tobytes() for i in keep})
+            assert np.array_equal(objects.reconstruct_object(many.chunks, fetched,
+                                                             contexts=ctxs), data)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_slices_cover_every_chunk_once():
+    for cnt in range(1, 40):
+        for parts in range(1, 12):
+            sl = objects._slices(cnt, parts)
+            assert len(sl) == min(cnt, parts)
+            assert sl[0][0] == 0 and sl[-1][1] == cnt
+            assert all(a < b for a, b in sl) and all(sl[i][1] == sl[i + 1][0]
+                                                      for i in range(len(sl) - 1))
+            sizes = [b - a for a, b in sl]
+            assert max(sizes) - min(sizes) <= 1

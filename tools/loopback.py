@@ -14,7 +14,7 @@ reconstructs with decode_chunk's rule (sort, first k) on the GPU
 chain, network-fetched crsqlite, >100-chunk channel hang,
 download.rs:26,500) -- see SURVEY.md fact 9.
 
-usage: python tools/loopback.py [--size BYTES] [--miners N]   (prints one JSON line)
+usage: python tools/loopback.py [--size BYTES] [--miners N] [--gpus G]   (one JSON line)
        python tools/loopback.py miner --store-port P --http-port Q --dir D
 """
 from __future__ import annotations
@@ -148,7 +148,11 @@ def run(a):
 
 def _run(a, miners):
     M = len(miners)
-    ctx = _lib.Context(-1)
+    # one context per GPU; chunks partition across them. With
+    # more contexts than devices they share devices (multi-GPU rehearsal).
+    ngpu = a.gpus or max(1, _lib.device_count())
+    ctxs = objects.device_contexts(ngpu)
+    ctx = ctxs[0]
     obj = splitmix_bytes(0x5709B + a.seed, a.size)
     chunks = objects.chunk_spans(a.size)
     chunk_size = chunks[0][1]
@@ -157,7 +161,7 @@ def _run(a, miners):
     # ---- upload: GPU encode + GPU piece ids (objects.encode_object: one
     # batched call per run of equal chunks), then the store framing
     t0 = time.perf_counter()
-    enc = objects.encode_object(obj, ctx)
+    enc = objects.encode_object(obj, contexts=ctxs)
     t_encode = time.perf_counter() - t0
 
     per_miner = [[] for _ in range(M)]
@@ -236,7 +240,7 @@ def _run(a, miners):
     # reconstruct_chunk per chunk (first k by index), batched per run of
     # equal chunks straight into the object buffer
     out = objects.reconstruct_object(enc.chunks, [gathered[ci] for ci in range(len(metas))],
-                                     ctx)
+                                     contexts=ctxs)
     t_decode = time.perf_counter() - t2
     t_download = time.perf_counter() - t1
     ok = bool(np.array_equal(out, obj))
@@ -255,7 +259,8 @@ def _run(a, miners):
         "upload_GiBps": round(a.size / GIB / t_upload, 3),
         "download_GiBps": round(a.size / GIB / t_download, 3),
         "end_to_end_GiBps": round(a.size / GIB / (t_upload + t_download), 3),
-        "device": ctx.device,
+        "devices": [c.device for c in ctxs], "contexts": len(ctxs),
+        "visible_gpus": _lib.device_count(),
     }
     return res
 
@@ -274,6 +279,9 @@ def main():
     p.add_argument("--miners", type=int, default=8)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--kill-seed", type=int, default=7)
+    p.add_argument("--gpus", type=int, default=0,
+                   help="contexts to spread the chunks over, one per GPU (0 = every "
+                        "visible GPU; more than visible = several per device)")
     a = p.parse_args()
     res = run(a)
     print(json.dumps(res), flush=True)
