@@ -113,7 +113,7 @@ def test_loopback_roundtrip_small(gpus):
     on a one-GPU box), the config-5 layout for 8 x MI355X."""
     import loopback
     res = loopback.run(argparse.Namespace(size=(24 << 20) + 12345, miners=4, seed=1,
-                                          kill_seed=7, gpus=gpus))
+                                          kill_seed=7, gpus=gpus, cold=False))
     assert res["bit_exact"]
     assert res["ack_mismatch"] == 0
     assert res["chunks_decoded_through_parity"] > 0
