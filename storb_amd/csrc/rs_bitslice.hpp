@@ -277,6 +277,9 @@ __device__ __forceinline__ void encode_tile(const ApplyArgs &a, uint32_t stripe,
 // Group size per geometry: whole k in flight where the registers allow it.
 template <int K, int N>
 struct BsTune {
+  // resident workgroups per CU (rs_kernels.hpp wg_cap): RS(16,8) 0.281 ->
+  // 0.275 ms at 3 (tools/occ_sweep.py, profiles/r1_occupancy.txt)
+  static constexpr int OCC = K == 16 ? 3 : 0;
   static constexpr int G = K <= 8 ? K : ((N - K) >= 16 ? 2 : 4);
 };
 
@@ -300,8 +303,8 @@ hipError_t launch_bitslice(const ApplyArgs &a, hipStream_t s) {
   const uint64_t blocks = ((cols + 511) / 512) * a.nstripes;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  hipLaunchKernelGGL((rs_encode_bitslice<K, N>), dim3(blocks), dim3(256), 0, s, a);
-  return hipGetLastError();
+  return launch_lds<rs_encode_bitslice<K, N>>(blocks, 256,
+                                               cap_lds(wg_cap(BsTune<K, N>::OCC), 0), s, a);
 }
 
 }  // namespace bs

@@ -42,8 +42,30 @@ static constexpr int kThreads = 256;
 // G = input shares per load group (double-buffered); TL = stage the
 // k*RM nibble tables in LDS at block start and read them as broadcast
 // ds_reads instead of s_loads.
+// Resident workgroups per CU (rs_kernels.hpp wg_cap; 0 = uncapped), from
+// the product-level sweep tools/occ_sweep.py (profiles/r1_occupancy.txt):
+// RS(4,2) encode / decode 6.40 -> 6.65 TB/s at 5, its one-row repair +5-7 %,
+// RS(16,2) decode (config 5) +13 % at 3, RS(16,1) repair +9 % at 4; RS(8,4)
+// encode and the 8-row k = 16 decode +2-4 % at 4 (tools/kbench_tune.hip occ).
+// RS(2,1) (Storb's own 256 KiB chunks) and config 3's <8,3> decode measured
+// best or even uncapped.
+constexpr int occ_for(int KM, int RM, bool copy) {
+  if (copy) {  // fused assembly: config 3's into-a-fresh-buffer decode, pure copy
+    if (KM == 8 && RM == 3) return 4;
+    if (KM == 8 && RM == 1) return 3;
+  }
+  if (KM == 4 && RM <= 2) return 5;
+  if (KM == 8 && RM == 4) return 4;
+  if (KM == 16 && RM == 1) return 4;
+  if (KM == 16 && RM == 2) return 3;
+  if (KM == 16 && RM == 8) return 4;
+  return 0;
+}
+
 template <int KM, int RM>
 struct Tune {
+  static constexpr int OCC = occ_for(KM, RM, false);
+  static constexpr int OCC_COPY = occ_for(KM, RM, true);
   static constexpr int T = 256;
   static constexpr int U = 1;
   static constexpr bool BAR = false;
@@ -292,22 +314,21 @@ __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
 }
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
-hipError_t launch_perm(const ApplyArgs &a, hipStream_t s) {
+hipError_t launch_perm(const ApplyArgs &a, hipStream_t s, int occ = 0, int occ_copy = 0) {
   const uint64_t cols = a.block >> 4;
   const uint64_t blocks = ((cols + T * U - 1) / (T * U)) * a.nstripes;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+  const size_t dyn = cap_lds(wg_cap(a.ncopy ? occ_copy : occ),
+                             TL ? sizeof(PermTab) * KM * RM : 0);
   if (a.ncopy) {
     if constexpr (KM <= static_cast<int>(kCopyMaxK))
-      hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR, true>), dim3(blocks),
-                         dim3(T), 0, s, a);
+      return launch_lds<rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR, true>>(blocks, T, dyn, s,
+                                                                             a);
     else
       return hipErrorInvalidValue;
-  } else {
-    hipLaunchKernelGGL((rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR>), dim3(blocks), dim3(T),
-                       0, s, a);
   }
-  return hipGetLastError();
+  return launch_lds<rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR>>(blocks, T, dyn, s, a);
 }
 
 template <int KM, int RM>
@@ -396,7 +417,7 @@ inline uint64_t tile_blocks(const ApplyArgs &a) {
 template <int KM, int RM>
 hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
   using C = Tune<KM, RM>;
-  return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s);
+  return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC, C::OCC_COPY);
 }
 
 template <int KM>

@@ -1,6 +1,8 @@
 // rs_kernels.hip -- dispatch, the any-alignment byte kernel and the
 // synthetic-input fill kernel. The dwordx4 kernels and their design notes
 // are in rs_device.hpp; their instantiations in rs_perm_k*.hip / rs_lds.hip.
+#include <cstdlib>
+
 #include "rs_device.hpp"
 
 namespace storb_rs {
@@ -67,6 +69,14 @@ __global__ __launch_bounds__(kThreads) void fill_splitmix_kernel(
       for (uint64_t b = 0; b < nb; b++) p[b] = static_cast<uint8_t>(z >> (8 * b));
     }
   }
+}
+
+int wg_cap_override() {
+  static const int v = [] {
+    const char *e = std::getenv("STORB_RS_WG_PER_CU");
+    return e && *e ? std::atoi(e) : -1;
+  }();
+  return v;
 }
 
 bool vector_ok(const ApplyArgs &a) {

@@ -2,7 +2,11 @@
 #pragma once
 
 #include <hip/hip_runtime_api.h>
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#endif
 
+#include <atomic>
 #include <cstdint>
 
 #include "gf256.hpp"
@@ -47,6 +51,48 @@ struct ApplyArgs {
 constexpr uint32_t kCopyMaxK = 16;
 
 enum class Variant { Perm = 1, Lds = 2 };
+
+// Workgroups resident per CU. The streaming kernels issue all their loads
+// up front; with every slot of a CU filled (8 workgroups of 256 lanes) more
+// DRAM pages are open at once than the HBM3E channels serve well, and
+// capping the resident workgroups streams faster (tools/kbench_tune.hip
+// "occ", profiles/r1_occupancy.txt). The cap is imposed by reserving LDS:
+// a workgroup asks for 160 KiB / cap, so cap fit on a CU and cap + 1 do not.
+// STORB_RS_WG_PER_CU overrides every kernel's cap (0 = uncapped).
+constexpr size_t kLdsPerCu = 160u << 10;
+int wg_cap_override();  // -1 when unset
+inline int wg_cap(int tuned) {
+  const int o = wg_cap_override();
+  return o >= 0 ? o : tuned;
+}
+// Dynamic LDS to request so at most `cap` workgroups with `static_lds`
+// bytes of static LDS each are resident on a CU (0 = no cap).
+inline size_t cap_lds(int cap, size_t static_lds) {
+  if (cap <= 0) return 0;
+  const size_t per = kLdsPerCu / static_cast<size_t>(cap) / 1024 * 1024;
+  return per > static_lds ? per - static_lds : 0;
+}
+
+#ifdef __HIPCC__
+// Launch kernel Kern with `dyn` bytes of dynamic LDS (the resident-workgroup
+// cap); above 64 KiB each kernel must opt in once.
+template <auto Kern>
+hipError_t launch_lds(uint64_t blocks, int threads, size_t dyn, hipStream_t s,
+                      const ApplyArgs &a) {
+  if (dyn > (64u << 10)) {
+    static std::atomic<size_t> opted{0};  // per kernel instantiation
+    if (opted.load(std::memory_order_relaxed) < dyn) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(Kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               static_cast<int>(dyn));
+      if (e != hipSuccess) return e;
+      opted.store(dyn, std::memory_order_relaxed);
+    }
+  }
+  hipLaunchKernelGGL(Kern, dim3(blocks), dim3(threads), dyn, s, a);
+  return hipGetLastError();
+}
+#endif
 
 // Smallest power of two >= v: the kernel bucket for k.
 inline int pow2_bucket(uint32_t v) {

@@ -69,12 +69,47 @@ V mk() {
            }, {}};
 }
 
+// Occupancy cap: the same kernel launched with dynamic LDS so only
+// `wg_per_cu` workgroups fit a CU's 160 KiB (does fewer waves in flight
+// stream HBM better? argv[3] = "occ").
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL = false, bool PAIR = false>
+V mk_occ(int wg_per_cu) {
+  V v = mk<KM, RM, T, U, BAR, G, TL, PAIR>();
+  // per-WG LDS (static tables + dynamic) = 160 KiB / n rounded down to 1 KiB:
+  // n workgroups fit a CU, n + 1 do not
+  const size_t stat = TL ? sizeof(PermTab) * KM * RM : 0;
+  const size_t lds = wg_per_cu ? ((160u << 10) / wg_per_cu) / 1024 * 1024 - stat : 0;
+  v.name += " wg/CU<=" + std::to_string(wg_per_cu);
+  v.fn = [lds](const ApplyArgs &a, hipStream_t s) {
+    auto kern = rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR>;
+    if (lds > (64u << 10)) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         static_cast<int>(lds));
+      if (e != hipSuccess) return e;
+    }
+    const uint64_t cols = a.block >> 4;
+    const uint64_t blocks = ((cols + T * U - 1) / (T * U)) * a.nstripes;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(T), lds, s, a);
+    return hipGetLastError();
+  };
+  return v;
+}
+
 template <int KM, int RM>
 V product() {
   using C = Tune<KM, RM>;
   V v = mk<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>();
   v.name = "product " + v.name;
   return v;
+}
+
+template <int KM, int RM>
+void add_occ(std::vector<V> &v) {
+  using C = Tune<KM, RM>;
+  v.push_back(product<KM, RM>());
+  for (int n : {2, 3, 4, 5, 6})
+    v.push_back(mk_occ<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(n));
 }
 
 template <int KM, int RM>
@@ -114,7 +149,21 @@ int main(int argc, char **argv) {
   ws[3].vs.back().name += " (r padded to 4)";
   ws[4].vs.push_back(product<8, 3>());
   ws[5].vs.push_back(product<8, 3>());
-  if (argc > 2) ws.erase(ws.begin(), ws.begin() + std::atoi(argv[2]));
+  if (argc > 3 && std::strcmp(argv[3], "occ") == 0) {  // occupancy sweep, product shapes
+    std::vector<W> o = {ws[0], ws[3], ws[2],
+                        {"W5 RS(16,2) decode 128 x 8 MiB (config 5 decode shape)", 16, 2, 128,
+                         512 << 10, {}},
+                        {"W6 RS(8,4) encode 4096 x 256 KiB", 8, 4, 4096, 32 << 10, {}}};
+    for (auto &w : o) w.vs.clear();
+    add_occ<4, 2>(o[0].vs);
+    add_occ<8, 3>(o[1].vs);
+    add_occ<16, 8>(o[2].vs);
+    add_occ<16, 2>(o[3].vs);
+    add_occ<8, 4>(o[4].vs);
+    ws = o;
+  } else if (argc > 2) {
+    ws.erase(ws.begin(), ws.begin() + std::atoi(argv[2]));
+  }
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
