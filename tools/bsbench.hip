@@ -24,6 +24,9 @@
 
 using namespace storb_rs;
 
+// The product reads STORB_RS_WG_PER_CU here (rs_kernels.hip).
+int storb_rs::wg_cap_override() { return -1; }
+
 #define CK(x)                                                                  \
   do {                                                                         \
     hipError_t e = (x);                                                        \

@@ -24,6 +24,10 @@
 
 using namespace storb_rs;
 
+// The product reads STORB_RS_WG_PER_CU here (rs_kernels.hip); this tool
+// sets every cap itself.
+int storb_rs::wg_cap_override() { return -1; }
+
 #define CK(x)                                                                  \
   do {                                                                         \
     hipError_t e = (x);                                                        \
@@ -108,7 +112,7 @@ template <int KM, int RM>
 void add_occ(std::vector<V> &v) {
   using C = Tune<KM, RM>;
   v.push_back(product<KM, RM>());
-  for (int n : {2, 3, 4, 5, 6})
+  for (int n : {0, 2, 3, 4, 5, 6})
     v.push_back(mk_occ<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(n));
 }
 
@@ -156,6 +160,10 @@ int main(int argc, char **argv) {
                         {"W6 RS(8,4) encode 4096 x 256 KiB", 8, 4, 4096, 32 << 10, {}}};
     for (auto &w : o) w.vs.clear();
     add_occ<4, 2>(o[0].vs);
+    for (int n : {8, 9, 10, 11, 12})  // finer caps: 128-lane workgroups
+      o[0].vs.push_back(mk_occ<4, 2, 128, 1, false, 4, false, false>(n));
+    for (int n : {16, 18, 20, 22, 24})  // one wave per workgroup
+      o[0].vs.push_back(mk_occ<4, 2, 64, 1, false, 4, false, false>(n));
     add_occ<8, 3>(o[1].vs);
     add_occ<16, 8>(o[2].vs);
     add_occ<16, 2>(o[3].vs);
