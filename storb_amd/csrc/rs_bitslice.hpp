@@ -278,8 +278,8 @@ __device__ __forceinline__ void encode_tile(const ApplyArgs &a, uint32_t stripe,
 template <int K, int N>
 struct BsTune {
   // resident workgroups per CU (rs_kernels.hpp wg_cap): RS(16,8) 0.281 ->
-  // 0.275 ms at 3 (tools/occ_sweep.py, profiles/r1_occupancy.txt)
-  static constexpr int OCC = K == 16 ? 3 : 0;
+  // 0.275 ms at 2 (= 3; tools/occ_sweep.py, profiles/r1_occupancy.txt)
+  static constexpr int OCC = K == 16 ? 2 : 0;
   static constexpr int G = K <= 8 ? K : ((N - K) >= 16 ? 2 : 4);
 };
 

@@ -44,20 +44,21 @@ static constexpr int kThreads = 256;
 // ds_reads instead of s_loads.
 // Resident workgroups per CU (rs_kernels.hpp wg_cap; 0 = uncapped), from
 // the product-level sweep tools/occ_sweep.py (profiles/r1_occupancy.txt):
-// RS(4,2) encode / decode 6.40 -> 6.65 TB/s at 5, its one-row repair +5-7 %,
-// RS(16,2) decode (config 5) +13 % at 3, RS(16,1) repair +9 % at 4; RS(8,4)
-// encode and the 8-row k = 16 decode +2-4 % at 4 (tools/kbench_tune.hip occ).
-// RS(2,1) (Storb's own 256 KiB chunks) and config 3's <8,3> decode measured
-// best or even uncapped.
+// RS(4,2) encode / decode 6.40 -> 6.65 TB/s at 4, its one-row repair +5-7 %,
+// RS(16,2) decode (config 5) +13 % at 2, RS(16,1) repair +9 % at 4; RS(8,4)
+// encode, config 3's <8,3> decode and the 8-row k = 16 decode +1-4 % at 4
+// (tools/kbench_tune.hip occ). RS(2,1) (Storb's own 256 KiB chunks) and the
+// k = 1 copy measured best uncapped. For 256-lane workgroups caps 2 and 3
+// measure the same, as do 4 and 5: the reservation resolves to even counts.
 constexpr int occ_for(int KM, int RM, bool copy) {
   if (copy) {  // fused assembly: config 3's into-a-fresh-buffer decode, pure copy
     if (KM == 8 && RM == 3) return 4;
-    if (KM == 8 && RM == 1) return 3;
+    if (KM == 8 && RM == 1) return 2;
   }
-  if (KM == 4 && RM <= 2) return 5;
-  if (KM == 8 && RM == 4) return 4;
+  if (KM == 4 && RM <= 2) return 4;
+  if (KM == 8 && (RM == 3 || RM == 4)) return 4;
   if (KM == 16 && RM == 1) return 4;
-  if (KM == 16 && RM == 2) return 3;
+  if (KM == 16 && RM == 2) return 2;
   if (KM == 16 && RM == 8) return 4;
   return 0;
 }

@@ -164,7 +164,17 @@ int main(int argc, char **argv) {
       o[0].vs.push_back(mk_occ<4, 2, 128, 1, false, 4, false, false>(n));
     for (int n : {16, 18, 20, 22, 24})  // one wave per workgroup
       o[0].vs.push_back(mk_occ<4, 2, 64, 1, false, 4, false, false>(n));
+    for (int n : {2, 3, 4})  // two columns per lane under a cap
+      o[0].vs.push_back(mk_occ<4, 2, 256, 2, false, 4, false, false>(n));
+    for (int n : {2, 3})
+      o[0].vs.push_back(mk_occ<4, 2, 512, 1, false, 4, false, false>(n));
     add_occ<8, 3>(o[1].vs);
+    for (int n : {0, 8, 10, 12, 16})
+      o[1].vs.push_back(mk_occ<8, 3, 128, 1, false, 8, true, true>(n));
+    for (int n : {0, 16, 20, 24, 32})
+      o[1].vs.push_back(mk_occ<8, 3, 64, 1, false, 8, true, true>(n));
+    for (int n : {0, 3, 4, 5})
+      o[1].vs.push_back(mk_occ<8, 3, 256, 1, false, 4, true, true>(n));
     add_occ<16, 8>(o[2].vs);
     add_occ<16, 2>(o[3].vs);
     add_occ<8, 4>(o[4].vs);
