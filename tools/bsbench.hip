@@ -64,6 +64,13 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, int tail) 
   vs.push_back({"bitslice", [](const ApplyArgs &a, hipStream_t s) {
                   return bs::launch_bitslice<K, N>(a, s);
                 }, {}});
+  for (int cap : {0, 2, 4, 6})  // resident-workgroup caps (rs_kernels.hpp wg_cap)
+    vs.push_back({"bitslice wg/CU<=" + std::to_string(cap),
+                  [cap](const ApplyArgs &a, hipStream_t s) {
+                    const uint64_t blocks = ((a.block / 16 + 511) / 512) * a.nstripes;
+                    return launch_lds<bs::rs_encode_bitslice<K, N>>(blocks, 256, cap_lds(cap, 0),
+                                                                   s, a);
+                  }, {}});
   B -= tail;  // ragged share size: exercises the guarded tail
   const uint64_t in_bytes = (uint64_t)nstripes * K * B, out_bytes = (uint64_t)nstripes * R * B;
   uint8_t *in, *out;
