@@ -21,8 +21,10 @@ Other BASELINE configs (not the driver's line):
   --config 4  10 000 x 1 MiB objects encoded, object i on rank i mod N
               (strong scaling: total work fixed)
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
+Launch: python bench.py [--gpus N --steps K --warmup W]. One rank per GPU:
+under torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env, which must agree
+with --gpus), or, with --gpus N > 1 and no WORLD_SIZE, this script spawns the
+N rank processes itself before touching the GPU (storb_amd/launch.py).
 """
 from __future__ import annotations
 
@@ -40,7 +42,7 @@ import torch.distributed as dist
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-from storb_amd import _lib, partition  # noqa: E402
+from storb_amd import _lib, launch, partition  # noqa: E402
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -120,7 +122,7 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
 
 
 def cpu_baseline_threads(k, n, chunk_bytes, erased, threads=16, nchunks=256, seconds=3.0):
-    """The same CPU path on `threads` host cores over independent chunks
+    """The same CPU path on `threads` host threads over independent chunks
     ("nproc threads on independent chunks"; 16 = this box's
     CPU share per GPU). Encode + decode round trips over `nchunks` distinct
     chunks, repeated until `seconds` have passed, bit-exact checked."""
@@ -142,6 +144,22 @@ def cpu_baseline_threads(k, n, chunk_bytes, erased, threads=16, nchunks=256, sec
             "cores": threads, "kind": "port",
             "sample": f"{passes} passes x {nchunks} x encode+decode of {chunk_bytes >> 10} KiB "
                       f"chunks, {threads} threads, {el:.2f} s"}
+
+
+def cpu_quota():
+    """The CPUs this process may actually use: affinity mask and the cgroup v2
+    CPU quota (cpu.max 'quota period'), which can be far below nproc."""
+    q = {"nproc": os.cpu_count()}
+    try:
+        q["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        q["affinity"] = None
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        q["cgroup_cpus"] = None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        q["cgroup_cpus"] = None
+    return q
 
 
 def cpu_model():
@@ -487,14 +505,32 @@ class Workload:
         return N * (k + e) * B
 
 
+def rank_info(rank, world, local, dev, backend):
+    """Who ran: every rank's GPU (ordinal + PCI bus) and the process group's
+    own rank count, so a scaling line cannot silently be a 1-rank number."""
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "device": local, "name": props.name,
+          "pci_bus": getattr(props, "pci_bus_id", None), "host": platform.node()}
+    if world == 1:
+        return {"world_size": 1, "backend": None, "pg_ranks": 1, "ranks": [me]}
+    ranks = [None] * world
+    dist.all_gather_object(ranks, me)
+    return {"world_size": world, "backend": dist.get_backend(),
+            "pg_ranks": dist.get_world_size(), "ranks": ranks,
+            "distinct_gpus": len({(r["host"], r["device"]) for r in ranks})}
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # One process per GPU. Decided before any GPU call: with --gpus N > 1 and
+    # no WORLD_SIZE in the environment this process only spawns the N ranks
+    # (storb_amd/launch.py); under torch.distributed.run it is one of them.
+    plan = launch.plan_launch(a.gpus, os.environ, torch.cuda.device_count(), a.dist_backend)
+    if plan.action == "spawn":
+        sys.exit(launch.spawn_ranks([os.path.abspath(__file__), *sys.argv[1:]], plan.world))
+    world, rank, local = plan.world, plan.rank, plan.device
     # STORB_BENCH_DEVICE pins every rank to one GPU (multi-rank rehearsal on a
     # single-GPU box with --dist-backend gloo); by default rank i uses GPU i.
-    local = int(os.environ.get("STORB_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -502,6 +538,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(a.dist_backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {world}")
+    ranks = rank_info(rank, world, local, dev, a.dist_backend)
 
     ctx = _lib.Context(local)
     ctx.set_kernel({"auto": _lib.KERNEL_AUTO, "perm": _lib.KERNEL_PERM,
@@ -626,6 +665,7 @@ def main():
             "survivors": w.survivors if w.erased else None, "kernel": a.kernel,
             "parallelism": f"independent objects, {world} GPU(s), no collectives",
         },
+        "launch": ranks,
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -651,9 +691,19 @@ def main():
                                                do_encode="encode" in w.legs,
                                                do_decode="decode" in w.legs)
             out["cpu_baseline"]["cpu_model"] = cpu_model()
-            if a.config == 2:
-                out["cpu_baseline_threads"] = cpu_baseline_threads(w.k, w.n, w.chunk,
-                                                                   set(w.erased))
+            if a.config in (2, 5):
+                # the same code on threads over independent
+                # chunks -- at this box's CPU share per GPU (16) and at
+                # nproc (every logical CPU the OS reports; the cgroup quota,
+                # if any, is stated beside it).
+                er = set(w.erased)
+                nch = max(32, (256 << 20) // w.chunk)
+                out["cpu_baseline_threads"] = cpu_baseline_threads(w.k, w.n, w.chunk, er,
+                                                                   threads=16, nchunks=nch)
+                nproc = os.cpu_count() or 1
+                out["cpu_baseline_nproc"] = cpu_baseline_threads(
+                    w.k, w.n, w.chunk, er, threads=nproc, nchunks=max(nch, nproc))
+                out["cpu_baseline_nproc"]["cpu_quota"] = cpu_quota()
         if not a.no_host_path and a.config in (2, 5):
             out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
                                                    nchunks=max(8, (256 << 20) // w.chunk),

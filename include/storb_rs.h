@@ -223,7 +223,9 @@ int storb_rs_fill_splitmix_dev(storb_rs_ctx *ctx, uint8_t *d, size_t obj_len,
 #define STORB_RS_KERNEL_LDS 2  /* 256-B product tables staged in LDS */
 int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant);
 
-/* Synchronise the context's stream(s). */
+/* Synchronise the context's own streams and the HIP null stream of its
+ * device (where device calls given hip_stream = NULL run). Work the caller
+ * queued on streams of its own is the caller's to synchronise. */
 int storb_rs_sync(storb_rs_ctx *ctx);
 
 #ifdef __cplusplus

@@ -213,8 +213,10 @@ class Context:
         if rc != OK:
             raise StorbRsError(rc, "storb_rs_ctx_create")
         self._h = h
-        # hipStream_t used when a call passes stream=None (None -> the
-        # context's own stream). Tests point it at torch's current stream.
+        # hipStream_t used when a call passes stream=None. None here means
+        # NULL at the ABI: the HIP null stream, which orders with torch's
+        # default stream and which sync() waits for. Tests point it at
+        # torch's current stream.
         self.default_stream: Optional[int] = None
 
     def _s(self, stream):

@@ -70,12 +70,29 @@ struct PinBuf {
 // Device-resident coefficient tables for one (rows x k) matrix, tiled in
 // kSlotR x kSlotK blocks: for block b, ptab + b_off[b] PermTabs and
 // btab + b_off[b]*256 product-table bytes.
+//
+// Nothing about a table blocks the host: the device copy is allocated
+// stream-ordered (hipMallocAsync) and uploaded on the first caller's stream
+// (`home`); a call on another stream waits for the `uploaded` event on the
+// device. Every stream that launches with the table re-records its own
+// `uses` event, so eviction (LRU, ctx->table_cap entries) can order the
+// hipFreeAsync after the last kernel that reads the table on any stream.
 struct Tables {
   uint8_t *dev = nullptr;
   size_t perm_bytes = 0;
   std::vector<size_t> b_off;
+  std::vector<uint8_t> host;      // upload source, kept until the table is evicted
+  hipStream_t home = nullptr;     // stream the upload was ordered on
+  hipEvent_t uploaded = nullptr;  // recorded on `home` after the upload
+  bool upload_done = false;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // last use per stream
+  uint64_t tick = 0;              // LRU clock
   ~Tables() {
+    // Context teardown only (its streams are drained first); eviction frees
+    // asynchronously instead (storb_rs.cpp evict_tables).
     if (dev) (void)hipFree(dev);
+    if (uploaded) (void)hipEventDestroy(uploaded);
+    for (auto &u : uses) (void)hipEventDestroy(u.second);
   }
 };
 
@@ -106,6 +123,8 @@ struct storb_rs_ctx {
   storb_rs::detail::PinBuf pin_in, pin_out;
   storb_rs::detail::PinBuf pipe_in[2], pipe_out[2];
   std::map<std::vector<uint8_t>, std::unique_ptr<storb_rs::detail::Tables>> tables;
+  size_t table_cap = 1024;  // cached matrices (STORB_RS_TABLE_CACHE), LRU-evicted
+  uint64_t table_tick = 0;
   std::unique_ptr<storb_rs::HostPool> pool;  // host copy workers, created on first use
   // Single-call paths whose staged bytes (in + out) are at most this size
   // run the kernel straight on the pinned staging buffers (zero-copy over
@@ -146,9 +165,11 @@ void blake3_host(const uint8_t *data, size_t len, uint8_t out[32]);
 // [p, p+len) inside one storb_rs_host_alloc / _register range.
 bool range_pinned(const void *p, size_t len);
 Variant pick_variant(const storb_rs_ctx *ctx);
-// Device tables of a rows x k coefficient matrix (cached per context).
+// Device tables of a rows x k coefficient matrix (cached per context), made
+// ready for launches on stream s; call tables_used() after those launches.
 int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
-               hipStream_t s, const Tables **out);
+               hipStream_t s, Tables **out);
+int tables_used(storb_rs_ctx *ctx, Tables *t, hipStream_t s);
 // out_r = sum_j coef[r][j] * in_j for every stripe, tiled onto kernel slots.
 // copy[j] != null (fused assembly, copy_fusable() true): input j is also
 // stored to copy[j] as the kernel reads it; rows may then be 0.
@@ -176,6 +197,10 @@ int repair_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                 const std::vector<uint32_t> &slot_idx, const uint32_t *targets,
                 uint32_t ntargets, std::vector<uint8_t> &coef);
 HostPool &host_pool(storb_rs_ctx *ctx);
+// Wait for everything queued on the context's own streams, ignoring errors
+// (the early-error paths of the host calls, whose kernels may still be
+// reading / writing the caller's page-locked buffers).
+void drain_streams(storb_rs_ctx *ctx);
 hipStream_t pick_stream(storb_rs_ctx *ctx, void *s);
 // Device address of page-locked host memory.
 hipError_t host_dev_ptr(uint8_t *host, uint8_t **dev);

@@ -21,11 +21,9 @@ extern "C" {
 // unpacks batch i-1 (hipMemcpyAsync from pinned memory is a true DMA).
 // With hashes_out, the blake3 of every share is computed on the device
 // right after the encode kernel and only the digests come back.
-static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                               const uint8_t *data, size_t chunk_len, uint32_t nchunks,
                               uint8_t *parity_out, uint8_t *hashes_out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
   if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
   if (chunk_len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
   const uint32_t p = n - k;
@@ -180,12 +178,10 @@ static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
 // double-buffered pinned pipeline as encode: pack the k survivors into
 // pinned staging (present data shares also go straight to `out`), H2D,
 // rebuild only the missing rows, D2H them, unpack into `out`.
-int storb_rs_decode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
-                           size_t padlen, uint32_t nchunks, const uint8_t *const *shares,
-                           const uint32_t *share_idx, const uint32_t *nshares, uint8_t *out,
-                           size_t out_stride) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                                size_t padlen, uint32_t nchunks, const uint8_t *const *shares,
+                                const uint32_t *share_idx, const uint32_t *nshares,
+                                uint8_t *out, size_t out_stride) {
   if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
   if (nchunks == 0) return STORB_RS_OK;
   if (!shares || !share_idx || !nshares || !out || block == 0 ||
@@ -311,6 +307,30 @@ int storb_rs_decode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t blo
     unpack(ii);
   }
   return STORB_RS_OK;
+}
+
+// On an early error, batches already queued may still read or write the
+// caller's buffers (page-locked ones in place): drain before returning.
+static int encode_chunks_impl(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                              size_t chunk_len, uint32_t nchunks, uint8_t *parity_out,
+                              uint8_t *hashes_out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const int rc = encode_chunks_locked(ctx, k, n, data, chunk_len, nchunks, parity_out, hashes_out);
+  if (rc) drain_streams(ctx);
+  return rc;
+}
+
+int storb_rs_decode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                           size_t padlen, uint32_t nchunks, const uint8_t *const *shares,
+                           const uint32_t *share_idx, const uint32_t *nshares, uint8_t *out,
+                           size_t out_stride) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const int rc = decode_chunks_locked(ctx, k, n, block, padlen, nchunks, shares, share_idx,
+                                      nshares, out, out_stride);
+  if (rc) drain_streams(ctx);
+  return rc;
 }
 
 int storb_rs_encode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,

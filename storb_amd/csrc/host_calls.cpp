@@ -64,11 +64,9 @@ int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)
 
 extern "C" {
 
-int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
                     size_t len, uint8_t *const *parity_out, size_t *block_out,
                     size_t *padlen_out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
   if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
   if (len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
   const size_t B = (len + k - 1) / k, pad = B * k - len;
@@ -160,11 +158,9 @@ int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *da
   return STORB_RS_OK;
 }
 
-int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
                     const uint32_t *share_idx, uint32_t nshares, size_t block,
                     size_t padlen, uint8_t *out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
   if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
   if (!shares || !share_idx || !out || block == 0 ||
       padlen >= static_cast<size_t>(k) * block)
@@ -285,11 +281,9 @@ int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
   return STORB_RS_OK;
 }
 
-int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+static int repair_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
                     const uint32_t *share_idx, uint32_t nshares, size_t block,
                     const uint32_t *targets, uint32_t ntargets, uint8_t *const *out) {
-  if (!ctx) return STORB_RS_EINVAL;
-  std::lock_guard<std::mutex> lk(ctx->mu);
   if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
   if (!shares || !share_idx || (ntargets && (!targets || !out)) || block == 0)
     return fail(ctx, STORB_RS_EINVAL, "repair: bad arguments");
@@ -334,6 +328,36 @@ int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *co
   for (uint32_t r = 0; r < ntargets; r++)
     std::memcpy(out[r], ctx->pin_out.p + static_cast<size_t>(r) * S, block);
   return STORB_RS_OK;
+}
+
+int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                    size_t len, uint8_t *const *parity_out, size_t *block_out,
+                    size_t *padlen_out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const int rc = encode_one(ctx, k, n, data, len, parity_out, block_out, padlen_out);
+  if (rc) drain_streams(ctx);  // queued work may still touch caller buffers
+  return rc;
+}
+
+int storb_rs_decode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+                    const uint32_t *share_idx, uint32_t nshares, size_t block,
+                    size_t padlen, uint8_t *out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const int rc = decode_one(ctx, k, n, shares, share_idx, nshares, block, padlen, out);
+  if (rc) drain_streams(ctx);  // queued work may still touch caller buffers
+  return rc;
+}
+
+int storb_rs_repair(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *shares,
+                    const uint32_t *share_idx, uint32_t nshares, size_t block,
+                    const uint32_t *targets, uint32_t ntargets, uint8_t *const *out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const int rc = repair_one(ctx, k, n, shares, share_idx, nshares, block, targets, ntargets, out);
+  if (rc) drain_streams(ctx);  // queued work may still touch caller buffers
+  return rc;
 }
 
 }  // extern "C"

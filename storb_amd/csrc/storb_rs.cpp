@@ -70,19 +70,72 @@ Variant pick_variant(const storb_rs_ctx *ctx) {
   return ctx->variant == STORB_RS_KERNEL_LDS ? Variant::Lds : Variant::Perm;
 }
 
+// Evict the least recently used table without blocking the host: the free
+// is ordered (on ctx->stream) after the upload and after the last launch
+// that read the table on every stream that used it.
+static int evict_tables(storb_rs_ctx *ctx) {
+  auto victim = ctx->tables.begin();
+  for (auto it = ctx->tables.begin(); it != ctx->tables.end(); ++it)
+    if (it->second->tick < victim->second->tick) victim = it;
+  Tables *t = victim->second.get();
+  HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, t->uploaded, 0));
+  for (auto &u : t->uses) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, u.second, 0));
+  HIP_TRY(ctx, hipFreeAsync(t->dev, ctx->stream));
+  t->dev = nullptr;
+  // The host source of the upload must outlive the copy; that copy is the
+  // oldest work on `home` this table has, long finished in practice.
+  HIP_TRY(ctx, hipEventSynchronize(t->uploaded));
+  ctx->tables.erase(victim);  // events are released once they complete
+  return STORB_RS_OK;
+}
+
+// Make t usable on stream s: a stream other than the upload's waits for it
+// on the device (once the upload is known complete, no wait is issued).
+static int tables_ready(storb_rs_ctx *ctx, Tables *t, hipStream_t s) {
+  if (t->upload_done || s == t->home) return STORB_RS_OK;
+  const hipError_t q = hipEventQuery(t->uploaded);
+  if (q == hipSuccess) {
+    t->upload_done = true;
+    return STORB_RS_OK;
+  }
+  if (q != hipErrorNotReady) return hip_fail(ctx, q, "hipEventQuery(tables)");
+  HIP_TRY(ctx, hipStreamWaitEvent(s, t->uploaded, 0));
+  return STORB_RS_OK;
+}
+
+int tables_used(storb_rs_ctx *ctx, Tables *t, hipStream_t s) {
+  for (auto &u : t->uses)
+    if (u.first == s) {
+      HIP_TRY(ctx, hipEventRecord(u.second, s));
+      return STORB_RS_OK;
+    }
+  hipEvent_t e = nullptr;
+  HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  t->uses.emplace_back(s, e);
+  HIP_TRY(ctx, hipEventRecord(e, s));
+  return STORB_RS_OK;
+}
+
 // Build (or fetch) the device tables of a rows x k coefficient matrix.
 int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
-               hipStream_t s, const Tables **out) {
+               hipStream_t s, Tables **out) {
   std::vector<uint8_t> key(8 + static_cast<size_t>(rows) * k);
   std::memcpy(key.data(), &k, 4);
   std::memcpy(key.data() + 4, &rows, 4);
   std::memcpy(key.data() + 8, coef, static_cast<size_t>(rows) * k);
   auto it = ctx->tables.find(key);
   if (it != ctx->tables.end()) {
-    *out = it->second.get();
+    Tables *t = it->second.get();
+    t->tick = ++ctx->table_tick;
+    int rc = tables_ready(ctx, t, s);
+    if (rc) return rc;
+    *out = t;
     return STORB_RS_OK;
   }
-  if (ctx->tables.size() > 4096) ctx->tables.clear();
+  while (!ctx->tables.empty() && ctx->tables.size() >= std::max<size_t>(ctx->table_cap, 1)) {
+    int rc = evict_tables(ctx);
+    if (rc) return rc;
+  }
   auto t = std::make_unique<Tables>();
   // Blocks in the order the launcher walks them; each block's tables are
   // [input][tab_rows] with tab_rows = rows_bucket(rows in block) and the
@@ -95,7 +148,8 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
                std::min<uint32_t>(kSlotK, k - cb);
     }
   t->perm_bytes = round_up(total * sizeof(PermTab), 256);
-  std::vector<uint8_t> host(t->perm_bytes + total * 256, 0);
+  std::vector<uint8_t> &host = t->host;
+  host.assign(t->perm_bytes + total * 256, 0);
   PermTab *pt = reinterpret_cast<PermTab *>(host.data());
   uint8_t *bt = host.data() + t->perm_bytes;
   const GF256 &g = gf();
@@ -113,11 +167,17 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
           for (int x = 0; x < 256; x++) bt[o * 256 + x] = g.mul(c, static_cast<uint8_t>(x));
         }
     }
-  hipError_t e = hipMalloc(reinterpret_cast<void **>(&t->dev), host.size());
-  if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(tables)");
+  HIP_TRY(ctx, hipEventCreateWithFlags(&t->uploaded, hipEventDisableTiming));
+  hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&t->dev), host.size(), s);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMallocAsync(tables)");
   e = hipMemcpyAsync(t->dev, host.data(), host.size(), hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(ctx, e, "upload tables");
+  if (e == hipSuccess) e = hipEventRecord(t->uploaded, s);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s);  // nothing may still read or write t's memory
+    return hip_fail(ctx, e, "upload tables");
+  }
+  t->home = s;
+  t->tick = ++ctx->table_tick;
   *out = t.get();
   ctx->tables.emplace(std::move(key), std::move(t));
   return STORB_RS_OK;
@@ -131,7 +191,7 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
           const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s,
           uint8_t *const *copy, const size_t *copy_stride) {
   if ((rows == 0 && !copy) || block == 0 || nstripes == 0) return STORB_RS_OK;
-  const Tables *t = nullptr;
+  Tables *t = nullptr;
   const std::vector<uint8_t> zero_row(k, 0);
   const uint32_t trows = rows ? rows : 1;  // pure assembly: one zero row of tables
   int rc = get_tables(ctx, k, trows, rows ? coef : zero_row.data(), s, &t);
@@ -162,9 +222,13 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
       a.block = block;
       a.nstripes = nstripes;
       a.accumulate = cb > 0 ? 1 : 0;
-      HIP_TRY(ctx, launch_apply(a, v, s));
+      const hipError_t e = launch_apply(a, v, s);
+      if (e != hipSuccess) {
+        (void)tables_used(ctx, t, s);  // earlier tiles may be queued
+        return hip_fail(ctx, e, "launch_apply");
+      }
     }
-  return STORB_RS_OK;
+  return tables_used(ctx, t, s);
 }
 
 // Whether a decode into a separate buffer can assemble the chunk inside the
@@ -325,6 +389,13 @@ HostPool &host_pool(storb_rs_ctx *ctx) {
   return *ctx->pool;
 }
 
+void drain_streams(storb_rs_ctx *ctx) {
+  DeviceGuard g(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto &p : ctx->pipe)
+    if (p) (void)hipStreamSynchronize(p);
+}
+
 // NULL is the HIP null stream (ordered with the device's legacy default
 // stream, which is also PyTorch's default stream), not the context's own.
 hipStream_t pick_stream(storb_rs_ctx *, void *s) {
@@ -386,6 +457,8 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   c->zc_max = 64ull << 20;
   if (const char *e = std::getenv("STORB_RS_ZC_MAX")) c->zc_max = std::strtoull(e, nullptr, 10);
   if (const char *e = std::getenv("STORB_RS_ZC_BATCH")) c->zc_batch = std::atoi(e) != 0;
+  if (const char *e = std::getenv("STORB_RS_TABLE_CACHE"))
+    c->table_cap = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) != hipSuccess) {
@@ -488,7 +561,9 @@ int storb_rs_host_free(void *p) {
 
 int storb_rs_host_register(void *p, size_t len) {
   if (!p || len == 0) return STORB_RS_EINVAL;
-  const hipError_t e = hipHostRegister(p, len, hipHostRegisterPortable);
+  // Mapped: the zero-copy kernels address registered ranges through
+  // hipHostGetDevicePointer, which needs a device mapping of the range.
+  const hipError_t e = hipHostRegister(p, len, hipHostRegisterPortable | hipHostRegisterMapped);
   if (e != hipSuccess) return e == hipErrorOutOfMemory ? STORB_RS_ENOMEM : STORB_RS_EDEVICE;
   std::lock_guard<std::mutex> lk(g_pin_mu);
   g_pinned[reinterpret_cast<uintptr_t>(p)] = {len, false};
@@ -514,6 +589,9 @@ int storb_rs_sync(storb_rs_ctx *ctx) {
   DeviceGuard g(ctx->device);
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   for (auto &p : ctx->pipe) HIP_TRY(ctx, hipStreamSynchronize(p));
+  // Device calls given hip_stream = NULL run on the HIP null stream, which
+  // the (non-blocking) context streams do not order with: wait for it too.
+  HIP_TRY(ctx, hipStreamSynchronize(nullptr));
   return STORB_RS_OK;
 }
 
