@@ -20,6 +20,9 @@ Other BASELINE configs (not the driver's line):
   --config 3  RS(8,4) [storb k=8,m=12] decode, 4096 x 256 KiB, erased {0,3,5}
   --config 4  10 000 x 1 MiB objects encoded, object i on rank i mod N
               (strong scaling: total work fixed)
+  --config 5  RS(16,8) [storb k=16,m=24]: 128 x 8 MiB chunks (a 1 GiB object)
+  --config 6  RS(32,16) [storb k=32,m=48]: 32 x 32 MiB chunks
+              (5/6: --erase E loses data shares 0..E-1 for the decode leg)
 
 Launch: python bench.py [--gpus N --steps K --warmup W]. One rank per GPU:
 under torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env, which must agree
@@ -55,9 +58,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
+    p.add_argument("--config", type=int, choices=[2, 3, 4, 5, 6], default=2,
                    help="BASELINE config; 5 = the device-resident GPU half of config 5 "
-                        "(1 GiB object -> 128 x 8 MiB chunks, storb k=16, m=24)")
+                        "(1 GiB object -> 128 x 8 MiB chunks, storb k=16, m=24); 6 = "
+                        "Storb's widest geometry (32 MiB chunks of 16-64 GiB objects, "
+                        "storb k=32, m=48), 32 chunks per GPU")
+    p.add_argument("--erase", type=int, default=None,
+                   help="configs 5/6: data shares 0..E-1 lost per chunk for the decode leg "
+                        "(default 2); E >= 3 takes the run-time-compiled bit-sliced decode")
     p.add_argument("--chunks", type=int, default=None, help="chunks per GPU (config 2/3)")
     p.add_argument("--objects", type=int, default=10000, help="total objects (config 4)")
     p.add_argument("--kernel", choices=["auto", "perm", "lds"], default="auto",
@@ -415,7 +423,8 @@ def kernel_names(kernel, w):
                            else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")
     if "decode" in w.legs:
         e = sum(1 for x in w.erased if x < w.k)
-        names["decode"] = f"rs_apply_{table}<{min(w.k, 32)},{e}>"
+        names["decode"] = (f"storb_bs_jit<{w.k},{e}> (hipRTC)" if w.jit_decode
+                           else f"rs_apply_{table}<{min(w.k, 32)},{e}>")
     return names
 
 
@@ -444,16 +453,30 @@ class Workload:
             self.scaling = "weak"
             self.workload = (f"RS(k=8,m=4) [storb k=8,m=12] decode, erased [0, 3, 5], "
                              f"survivors first 8 by index, {N} x 256 KiB chunks per GPU")
-        elif c == 5:
-            self.k, self.n, chunk, self.erased = 16, 24, 8 << 20, [0, 1]
-            N = a.chunks or 128
+        elif c in (5, 6):
+            E = 2 if a.erase is None else a.erase
+            if c == 5:
+                self.k, self.n, chunk = 16, 24, 8 << 20
+                N = a.chunks or 128
+                what = "8 MiB chunks (a 1 GiB object)"
+                self.metric = ("GiB/s device-resident RS encode+decode, 8 MiB chunks k=16 m=8 "
+                               "(Storb's geometry for a 1 GiB object)")
+            else:
+                self.k, self.n, chunk = 32, 48, 32 << 20
+                N = a.chunks or 32
+                what = "32 MiB chunks (objects of 16-64 GiB)"
+                self.metric = ("GiB/s device-resident RS encode+decode, 32 MiB chunks k=32 m=16 "
+                               "(Storb's widest geometry)")
+            if not 0 < E <= self.n - self.k:
+                raise SystemExit(f"--erase must be in 1..{self.n - self.k}")
+            self.erased = list(range(E))
+            self.metric += f", {E} data shares lost"
             seed0 = SEED_BASE + rank * N
             self.legs = ("encode", "decode")
-            self.metric = ("GiB/s device-resident RS encode+decode, 8 MiB chunks k=16 m=8 "
-                           "(Storb's geometry for a 1 GiB object)")
             self.scaling = "weak"
-            self.workload = (f"RS(k=16,m=8) [storb k=16,m=24] encode + decode(erased [0, 1]) "
-                             f"of {N} x 8 MiB chunks (a 1 GiB object) per GPU, device-resident")
+            self.workload = (f"RS(k={self.k},m={self.n - self.k}) [storb k={self.k},m={self.n}] "
+                             f"encode + decode(erased {self.erased}) of {N} x {what} per GPU, "
+                             f"device-resident")
         else:
             self.k, self.n, chunk, self.erased = 4, 6, 1 << 20, []
             mine = partition.objects_for_rank(a.objects, rank, world)
@@ -466,6 +489,7 @@ class Workload:
             self.workload = (f"{a.objects} x 1 MiB objects, object i on rank i mod {world}; "
                              f"this rank {N} objects, one batched launch per step")
         self.chunk, self.N = chunk, N
+        self.jit_decode = False
         k, n = self.k, self.n
         self.B = chunk // k
         self.survivors = [i for i in range(n) if i not in self.erased][:k]
@@ -567,6 +591,14 @@ def main():
             raise SystemExit("decode round trip mismatch")
         del ref
 
+    # A decode matrix the table kernel is VALU-bound on gets its own compiled
+    # bit-sliced kernel (rs_jit.cpp); the first decode queued its compile.
+    # Let it finish so the timed steps run what a steady-state download runs.
+    if "decode" in w.legs:
+        w.decode()
+        stream.synchronize()
+        _lib.jit_wait()
+    jit0 = _lib.jit_stats()
     legs = [getattr(w, leg) for leg in w.legs]
     for _ in range(a.warmup):
         for f in legs:
@@ -600,6 +632,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = e_start.elapsed_time(e_end) / a.steps
+    jit1 = _lib.jit_stats()
+    w.jit_decode = jit1["launches"] - jit0["launches"] >= a.steps + a.warmup
     if not each:
         # Per-leg split (which kernel took what) from an untimed pass of the
         # same steps with an event after every leg; reported, not used for
@@ -681,6 +715,9 @@ def main():
                               "separate untimed pass with an event after every leg"),
             "alg_bytes_per_launch": alg,
             "copy_ceiling_gbs": None,
+            "jit": {"launches_in_run": jit1["launches"] - jit0["launches"],
+                    "compiled": jit1["compiled"], "compile_ms": round(jit1["compile_ms"], 1),
+                    "fallbacks": jit1["fallbacks"]},
         },
         "cpu_baseline": None,
     }
@@ -691,7 +728,7 @@ def main():
                                                do_encode="encode" in w.legs,
                                                do_decode="decode" in w.legs)
             out["cpu_baseline"]["cpu_model"] = cpu_model()
-            if a.config in (2, 5):
+            if a.config in (2, 5, 6):
                 # the same code on threads over independent
                 # chunks -- at this box's CPU share per GPU (16) and at
                 # nproc (every logical CPU the OS reports; the cgroup quota,
@@ -704,11 +741,11 @@ def main():
                 out["cpu_baseline_nproc"] = cpu_baseline_threads(
                     w.k, w.n, w.chunk, er, threads=nproc, nchunks=max(nch, nproc))
                 out["cpu_baseline_nproc"]["cpu_quota"] = cpu_quota()
-        if not a.no_host_path and a.config in (2, 5):
+        if not a.no_host_path and a.config in (2, 5, 6):
             out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
                                                    nchunks=max(8, (256 << 20) // w.chunk),
                                                    erased=[e for e in w.erased if e < w.k])
-        if a.config in (2, 5):
+        if a.config in (2, 5, 6):
             out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
             out["repair"] = repair_rate(ctx, w, stream)
         if a.config == 3:

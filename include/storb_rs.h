@@ -223,6 +223,34 @@ int storb_rs_fill_splitmix_dev(storb_rs_ctx *ctx, uint8_t *d, size_t obj_len,
 #define STORB_RS_KERNEL_LDS 2  /* 256-B product tables staged in LDS */
 int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant);
 
+/* Run-time-compiled bit-sliced kernels. Decode and repair apply rows of the
+ * inverted survivor matrix, known only when the erasure pattern is. Under
+ * AUTO, a matrix the table kernel would be VALU-bound on (k >= 8 and enough
+ * rows: RS(16, >= 3 missing), RS(32, >= 3), RS(8, >= 4); batches >= 4 MiB)
+ * gets its own bit-sliced kernel, compiled with hipRTC on a background thread
+ * and cached for the process; calls made while it compiles run the table
+ * kernel. STORB_RS_JIT=0 disables, =sync compiles before the first launch;
+ * STORB_RS_JIT_MAX caps the number of kernels (default 256). */
+typedef struct {
+  uint64_t compiled;  /* kernels compiled and cached */
+  uint64_t failed;    /* compiles that failed (those matrices use the table kernel) */
+  uint64_t pending;   /* compiles queued or running */
+  uint64_t launches;  /* launches of compiled kernels */
+  uint64_t fallbacks; /* wanted a compiled kernel, ran the table kernel */
+  double compile_ms;  /* total compile wall time */
+} storb_rs_jit_stats_t;
+int storb_rs_jit_stats(storb_rs_jit_stats_t *out);
+/* Block until no compile is pending (benchmarks and tests). */
+int storb_rs_jit_wait(void);
+/* Ahead of the calls: queue (wait != 0: finish) the compile of the decode
+ * kernel for one erasure pattern -- the shares offered, first k by index as
+ * in decode_batch_dev; assemble != 0 for a decode into a separate chunk
+ * buffer, 0 for in place. Only matrices the policy above wants are compiled
+ * (the call is a no-op otherwise). Needs no GPU. EDEVICE if the compile
+ * failed. */
+int storb_rs_jit_prepare_decode(uint32_t k, uint32_t n, const uint32_t *share_idx,
+                                uint32_t nshares, int assemble, int wait);
+
 /* Synchronise the context's own streams and the HIP null stream of its
  * device (where device calls given hip_stream = NULL run). Work the caller
  * queued on streams of its own is the caller's to synchronise. */

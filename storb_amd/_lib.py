@@ -48,6 +48,12 @@ vp = C.c_void_p
 sz = C.c_size_t
 
 
+class JitStats(C.Structure):
+    """storb_rs_jit_stats_t (include/storb_rs.h)."""
+    _fields_ = [("compiled", C.c_uint64), ("failed", C.c_uint64), ("pending", C.c_uint64),
+                ("launches", C.c_uint64), ("fallbacks", C.c_uint64), ("compile_ms", C.c_double)]
+
+
 def _declare(L):
     L.storb_rs_version.restype = C.c_char_p
     L.storb_rs_strerror.restype = C.c_char_p
@@ -103,6 +109,10 @@ def _declare(L):
     L.storb_rs_host_is_pinned.argtypes = [vp, sz]
     L.storb_rs_set_kernel.argtypes = [vp, C.c_int]
     L.storb_rs_sync.argtypes = [vp]
+    L.storb_rs_jit_stats.argtypes = [C.POINTER(JitStats)]
+    L.storb_rs_jit_wait.argtypes = []
+    L.storb_rs_jit_prepare_decode.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
+                                              C.c_uint32, C.c_int, C.c_int]
 
 
 def lib():
@@ -172,6 +182,30 @@ def _as_u8(data) -> np.ndarray:
     if isinstance(data, memoryview) and data.contiguous:
         return np.frombuffer(data.cast("B"), dtype=np.uint8)  # zero-copy view
     return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+def jit_stats() -> dict:
+    """Counters of the run-time-compiled bit-sliced kernels (rs_jit.cpp)."""
+    st = JitStats()
+    rc = lib().storb_rs_jit_stats(C.byref(st))
+    if rc != OK:
+        raise StorbRsError(rc, "storb_rs_jit_stats")
+    return {f: getattr(st, f) for f, _ in JitStats._fields_}
+
+
+def jit_wait():
+    """Block until no kernel compile is pending."""
+    lib().storb_rs_jit_wait()
+
+
+def jit_prepare_decode(k: int, n: int, share_idx: Sequence[int], assemble: bool = False,
+                       wait: bool = True):
+    """Compile (or queue) the decode kernel of one erasure pattern ahead of
+    the calls that need it; no GPU needed."""
+    ids = (C.c_uint32 * max(len(share_idx), 1))(*share_idx)
+    rc = lib().storb_rs_jit_prepare_decode(k, n, ids, len(share_idx), int(assemble), int(wait))
+    if rc != OK:
+        raise StorbRsError(rc, "storb_rs_jit_prepare_decode")
 
 
 class PinnedBuffer:

@@ -171,15 +171,12 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
                hipStream_t s, Tables **out);
 int tables_used(storb_rs_ctx *ctx, Tables *t, hipStream_t s);
 // out_r = sum_j coef[r][j] * in_j for every stripe, tiled onto kernel slots.
-// copy[j] != null (fused assembly, copy_fusable() true): input j is also
-// stored to copy[j] as the kernel reads it; rows may then be 0.
+// copy[j] != null (decode into a separate buffer): input j is also stored
+// to copy[j] (by the kernel where it can, else copied first); rows may be 0.
 int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
           const uint8_t *const *d_in, const size_t *in_stride, uint8_t *const *d_out,
           const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s,
           uint8_t *const *copy = nullptr, const size_t *copy_stride = nullptr);
-bool copy_fusable(const storb_rs_ctx *ctx, uint32_t k, size_t block,
-                  const uint8_t *const *d_in, const size_t *in_stride, size_t out_stride,
-                  const uint8_t *d_out);
 // Parity rows of (k, n): the bit-sliced encoder where compiled in, else apply.
 int encode_apply(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *d_in,
                  const size_t *in_stride, uint8_t *const *d_out, const size_t *out_stride,

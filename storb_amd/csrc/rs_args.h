@@ -1,0 +1,68 @@
+// rs_args.h -- the launch argument block of the GF(2^8) shard kernels.
+//
+// Self-contained on purpose: besides the ahead-of-time kernels it is handed
+// to hipRTC (as an in-memory header) for the per-matrix bit-sliced kernels
+// compiled at run time (rs_jit.cpp), so the JIT kernels read exactly the
+// struct the host fills in. No standard headers under hipRTC.
+#pragma once
+
+#ifdef __HIPCC_RTC__
+typedef unsigned char uint8_t;
+typedef unsigned int uint32_t;
+typedef unsigned long long uint64_t;
+#else
+#include <cstdint>
+#endif
+
+namespace storb_rs {
+
+struct PermTab;  // gf256.hpp (host side only)
+
+// One launch applies a (r x k) coefficient block to k input share slots and
+// writes (or XOR-accumulates into) r output share slots, for every stripe.
+// Larger matrices are tiled over several launches by the host (storb_rs.cpp).
+constexpr int kSlotK = 32;
+constexpr int kSlotR = 16;
+
+// Largest k bucket with COPY instantiations of the table kernel; wider
+// decodes copy survivors with hipMemcpy2DAsync before the kernel.
+constexpr uint32_t kCopyMaxK = 16;
+
+struct ApplyArgs {
+  const uint8_t *in[kSlotK];
+  uint64_t in_stride[kSlotK];
+  uint8_t *out[kSlotR];
+  uint64_t out_stride[kSlotR];
+  const PermTab *ptab;  // nibble tables [col][tab_rows], rows >= r zeroed
+  const uint8_t *btab;  // 256-byte product tables, same order (LDS variant)
+  uint32_t k, r;
+  uint32_t tab_rows;    // row stride of both tables = rows_bucket(r)
+  uint64_t block;       // bytes per share
+  uint32_t nstripes;
+  uint32_t accumulate;  // 1: out ^= result (column tiling), 0: out = result
+  // Fused assembly (decode into a separate chunk buffer): input slot j is
+  // also stored, as loaded, to copy[j] (null = not copied). ncopy > 0 selects
+  // the COPY kernels; r may then be 0 (pure assembly).
+  uint32_t ncopy;
+  uint8_t *copy[kSlotK];
+  uint64_t copy_stride[kSlotK];
+};
+
+// Launch shape of the bit-sliced kernels (rs_bitslice_core.h), shared by
+// the host launchers and the kernels. Grid: nstripes x tiles; a tile = 256
+// lanes x 32 B = 8 KiB of every share. Wave w of the tile covers 2 KiB: lane
+// l holds the 16-B columns (w*128 + l) and (w*128 + 64 + l) of the tile, so
+// each load and store instruction moves one contiguous 1 KiB per wave.
+namespace bs {
+constexpr int kBsThreads = 256;
+constexpr unsigned kBsColsPerTile = 512;
+
+// Shares per load group: whole k in flight where the registers allow it
+// (R x 8 accumulators + 2 x G x 8 loaded dwords + 30 table entries).
+constexpr int bs_group(int K, int R) {
+  return K <= 8 ? K
+                : (R >= 12 ? (K % 2 == 0 ? 2 : 1) : (K % 4 == 0 ? 4 : (K % 2 == 0 ? 2 : 1)));
+}
+}  // namespace bs
+
+}  // namespace storb_rs

@@ -1,0 +1,231 @@
+// rs_bitslice_core.h -- bit-sliced GF(2^8) matrix application with the
+// matrix compiled in, for any (R x K) matrix type M.
+//
+// Two users:
+//  * rs_bitslice.hpp: the ahead-of-time encoders for Storb's wide
+//    full-chunk geometries (k, n) = (16, 24), (32, 48) -- M = the generator's
+//    parity rows, computed constexpr;
+//  * rs_jit.cpp: decode / repair matrices known only at run time (rows of the
+//    inverted survivor matrix, piece.rs:384-386 Fec::decode) -- the host
+//    writes M out as a constexpr table and compiles this header with hipRTC,
+//    once per matrix, keeping the v_perm kernel for the calls that arrive
+//    while it compiles.
+// Self-contained (no standard headers) so hipRTC takes it as an in-memory
+// header next to rs_args.h.
+//
+// Method: a lane holds 32 bytes of a share (two dwordx4 loads,
+// each a contiguous 1 KiB per wave); a 3-layer SWAPMOVE network turns the 8
+// dwords into 8 bit-planes; multiplication by a constant is then a fixed 8x8
+// GF(2) bit matrix. Per input the 15 XOR combinations of planes 0-3 and of
+// planes 4-7 are formed (Method of Four Russians) and every output plane row
+// is acc ^= LO[row & 15] ^ HI[row >> 4]: one v_bitop3_b32 per (output,
+// plane, input) for 32 bytes. Outputs go back through the (involutive)
+// network before the stores.
+//
+// M provides: static constexpr int K, R; static constexpr unsigned long long
+// copy_mask (bit j: input j is also stored, as loaded, to a.copy[j] -- fused
+// assembly of a decode into a separate chunk buffer); static constexpr
+// <struct> net with net.row[R][K][8], where bit b' of row[p][j][b] is bit b
+// of M[p][j] * 2^b'.
+#pragma once
+
+#include "rs_args.h"
+
+#ifndef STORB_RS_NT_STORES
+#define STORB_RS_NT_STORES 1
+#endif
+
+namespace storb_rs {
+namespace bs {
+
+typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+
+// Compile-time loop: f(ic<I>) for I in [0, N). The network's indices must
+// be constants; #pragma unroll gives up on bodies this large and falls back
+// to dynamic VGPR indexing.
+template <typename T, T... I>
+struct iseq {};
+template <int I>
+struct ic {
+  static constexpr int value = I;
+};
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, iseq<int, I...>) {
+  (f(ic<I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+  static_for_impl(f, __make_integer_seq<iseq, int, N>{});
+}
+
+// (m & x) | (~m & y) as one v_bitop3_b32 (truth table over the operand
+// constants 0xF0/0xCC/0xAA, as LLVM encodes it). Written as the builtin so
+// InstCombine cannot re-split the selects of consecutive layers into extra
+// v_and_b32s (it did: +15 ops per transpose).
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t x, uint32_t y) {
+  return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
+}
+
+// Exchange bit S of the position with bit log2(S) of the register index
+// between registers lo (index bit clear) and hi (index bit set): 4 VALU ops.
+template <int S, uint32_t Mk>
+__device__ __forceinline__ void swapmove(uint32_t &lo, uint32_t &hi) {
+  const uint32_t l = lo, h = hi;
+  lo = sel(Mk << S, h << S, l);
+  hi = sel(Mk, l >> S, h);
+}
+
+// 8 dwords (32 bytes; byte q of dword r at bit 8q..8q+7 of x[r]) <-> 8
+// bit-planes (bit b of byte q of dword r at bit 8q + r of x[b]). The three
+// layers act on disjoint index bits, so the network is its own inverse.
+__device__ __forceinline__ void transpose8(uint32_t (&x)[8]) {
+  swapmove<1, 0x55555555u>(x[0], x[1]);
+  swapmove<1, 0x55555555u>(x[2], x[3]);
+  swapmove<1, 0x55555555u>(x[4], x[5]);
+  swapmove<1, 0x55555555u>(x[6], x[7]);
+  swapmove<2, 0x33333333u>(x[0], x[2]);
+  swapmove<2, 0x33333333u>(x[1], x[3]);
+  swapmove<2, 0x33333333u>(x[4], x[6]);
+  swapmove<2, 0x33333333u>(x[5], x[7]);
+  swapmove<4, 0x0F0F0F0Fu>(x[0], x[4]);
+  swapmove<4, 0x0F0F0F0Fu>(x[1], x[5]);
+  swapmove<4, 0x0F0F0F0Fu>(x[2], x[6]);
+  swapmove<4, 0x0F0F0F0Fu>(x[3], x[7]);
+}
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ v4 ld_nt(const v4 *p) { return __builtin_nontemporal_load(p); }
+// Stores: non-temporal unless STORB_RS_NT_STORES=0 (shares are touched once;
+// nt stores measured 5-9 % faster in steady state, profiles/r1_store_policy.txt).
+__device__ __forceinline__ void st_nt(v4 *p, v4 v) {
+#if STORB_RS_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+// One share's 32 bytes (already bit-sliced) folded into the R x 8
+// accumulator planes with the Four-Russians tables.
+template <class M, int J>
+__device__ __forceinline__ void fold_planes(uint32_t (&acc)[M::R][8], const uint32_t (&x)[8]) {
+  uint32_t lo[16], hi[16];
+  lo[0] = 0;
+  hi[0] = 0;
+#pragma unroll
+  for (int m = 1; m < 16; m++) {
+    const int b = __builtin_ctz(m), rest = m & (m - 1);
+    lo[m] = rest ? lo[rest] ^ x[b] : x[b];
+    hi[m] = rest ? hi[rest] ^ x[4 + b] : x[4 + b];
+  }
+#pragma unroll
+  for (int p = 0; p < M::R; p++) {
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int row = M::net.row[p][J][b];
+      const int l = row & 15, h = row >> 4;
+      if (l && h)
+        acc[p][b] = x3(acc[p][b], lo[l], hi[h]);
+      else if (l)
+        acc[p][b] ^= lo[l];
+      else if (h)
+        acc[p][b] ^= hi[h];
+    }
+  }
+}
+
+// The loads of one group of G shares: 2 x dwordx4 per share and lane, at the
+// lane's two (clamped) column indices ca / cb.
+template <int G>
+__device__ __forceinline__ void load_group(const ApplyArgs &a, int j0, uint32_t stripe,
+                                           uint32_t ca, uint32_t cb, v4 (&buf)[G][2]) {
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+    const v4 *p = reinterpret_cast<const v4 *>(a.in[j0 + g] +
+                                               static_cast<uint64_t>(stripe) * a.in_stride[j0 + g]);
+    buf[g][0] = ld_nt(p + ca);
+    buf[g][1] = ld_nt(p + cb);
+  }
+}
+
+// Accumulators pass through an empty volatile asm after every share, so the
+// Reassociate pass cannot regroup the 16-32 term XOR chains across shares
+// (which kept many shares' tables alive: 424 VGPRs at k = 16 without it).
+template <int R>
+__device__ __forceinline__ void fence_acc(uint32_t (&acc)[R][8]) {
+#pragma unroll
+  for (int p = 0; p < R; p++)
+    asm volatile("" : "+v"(acc[p][0]), "+v"(acc[p][1]), "+v"(acc[p][2]), "+v"(acc[p][3]),
+                 "+v"(acc[p][4]), "+v"(acc[p][5]), "+v"(acc[p][6]), "+v"(acc[p][7]));
+}
+
+// Shares are consumed in groups of G; group i+1's loads are issued before
+// group i is folded (double buffer). Ragged last tile: lanes past the share
+// end load a clamped (valid) column and store nothing. Bit-slicing keeps
+// every byte in its own bit position, so the garbage never reaches a stored
+// byte -- one branch-free body for full and partial tiles.
+template <class M, int G>
+__device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uint32_t v0,
+                                        uint32_t cols) {
+  constexpr int K = M::K, R = M::R;
+  static_assert(K % G == 0, "group size must divide k");
+  uint32_t acc[R][8];
+#pragma unroll
+  for (int p = 0; p < R; p++)
+#pragma unroll
+    for (int b = 0; b < 8; b++) acc[p][b] = 0;
+
+  v4 buf[2][G][2];
+  const uint32_t ca = v0 < cols ? v0 : cols - 1, cb = v0 + 64 < cols ? v0 + 64 : cols - 1;
+  load_group<G>(a, 0, stripe, ca, cb, buf[0]);
+  static_for<K / G>([&](auto GI) {
+    constexpr int gi = decltype(GI)::value;
+    if constexpr (gi + 1 < K / G)
+      load_group<G>(a, (gi + 1) * G, stripe, ca, cb, buf[(gi + 1) & 1]);
+    static_for<G>([&](auto GG) {
+      constexpr int g = decltype(GG)::value;
+      constexpr int j = gi * G + g;
+      const v4 &A = buf[gi & 1][g][0], &Bv = buf[gi & 1][g][1];
+      if constexpr (((M::copy_mask >> j) & 1ull) != 0) {
+        v4 *c = reinterpret_cast<v4 *>(a.copy[j] + static_cast<uint64_t>(stripe) * a.copy_stride[j]);
+        if (v0 < cols) st_nt(c + v0, A);
+        if (v0 + 64 < cols) st_nt(c + v0 + 64, Bv);
+      }
+      uint32_t x[8] = {A[0], A[1], A[2], A[3], Bv[0], Bv[1], Bv[2], Bv[3]};
+      // Ordering point: share j's bit-slicing cannot be hoisted above the
+      // previous share's fold, which bounds the live tables to one share.
+      asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                   "+v"(x[6]), "+v"(x[7]));
+      transpose8(x);
+      fold_planes<M, j>(acc, x);
+      fence_acc(acc);
+    });
+  });
+
+#pragma unroll
+  for (int p = 0; p < R; p++) {
+    transpose8(acc[p]);
+    v4 *q = reinterpret_cast<v4 *>(a.out[p] + static_cast<uint64_t>(stripe) * a.out_stride[p]);
+    const v4 A = {acc[p][0], acc[p][1], acc[p][2], acc[p][3]};
+    const v4 Bv = {acc[p][4], acc[p][5], acc[p][6], acc[p][7]};
+    if (v0 < cols) st_nt(q + v0, A);
+    if (v0 + 64 < cols) st_nt(q + v0 + 64, Bv);
+  }
+}
+
+// Grid: nstripes x tiles of kBsColsPerTile 16-B columns (rs_args.h).
+template <class M, int G>
+__device__ __forceinline__ void bs_kernel_body(const ApplyArgs &a) {
+  const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
+  const uint32_t tps = (cols + kBsColsPerTile - 1) / kBsColsPerTile;
+  const uint32_t stripe = blockIdx.x / tps;
+  const uint32_t tile = blockIdx.x - stripe * tps;
+  const uint32_t v0 = tile * kBsColsPerTile + (threadIdx.x >> 6) * 128 + (threadIdx.x & 63);
+  bs_tile<M, G>(a, stripe, v0, cols);
+}
+
+}  // namespace bs
+}  // namespace storb_rs

@@ -1,0 +1,366 @@
+// rs_jit.cpp -- bit-sliced kernels for matrices known only at run time.
+//
+// Decode (Fec::decode, piece.rs:384-386) and repair apply rows of the
+// inverted survivor matrix, which depend on which shares survived. The
+// v_perm table kernel takes any matrix but spends ~5.6 VALU ops per
+// (input, output, dword); from ~3 missing rows at k = 16 (the loss of 3+
+// miners per chunk for objects of 1 GiB and up) it is VALU-bound at 27-50 %
+// of HBM peak (profiles/r1_bsbench.txt). The bit-sliced method needs the
+// matrix as compile-time constants (rs_bitslice_core.h), so here the host
+// writes the matrix out as a constexpr table and compiles the same core
+// header with hipRTC, once per (matrix, copy mask), on a background thread.
+// Calls that arrive while a kernel compiles run the table kernel
+// (STORB_RS_JIT=sync waits instead); compiled kernels stay loaded for the
+// life of the process (never unloaded, so no queued launch can outlive its
+// code object), at most STORB_RS_JIT_MAX of them (default 256).
+#include <hip/hip_runtime_api.h>
+#include <hip/hiprtc.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/storb_rs.h"
+#include "gf256.hpp"
+#include "rs_jit.hpp"
+#include "rs_kernels.hpp"
+
+namespace storb_rs {
+namespace jit {
+namespace {
+
+// The header texts hipRTC compiles (generated from rs_args.h and
+// rs_bitslice_core.h by the Makefile, so they cannot drift from the
+// ahead-of-time kernels).
+#include "jit_headers.inc"
+
+enum class Mode { Off, Async, Sync };
+
+Mode mode() {
+  static const Mode m = [] {
+    const char *e = std::getenv("STORB_RS_JIT");
+    if (!e || !*e) return Mode::Async;
+    if (std::strcmp(e, "sync") == 0) return Mode::Sync;
+    return std::atoi(e) ? Mode::Async : Mode::Off;
+  }();
+  return m;
+}
+
+size_t max_kernels() {
+  static const size_t v = [] {
+    const char *e = std::getenv("STORB_RS_JIT_MAX");
+    return e && *e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : size_t{256};
+  }();
+  return v;
+}
+
+struct Entry {
+  enum State { Pending, Ready, Failed };
+  State state = Pending;
+  std::string src;
+  std::vector<char> code;
+  std::string log;
+  std::map<int, hipFunction_t> fn;  // per device
+  std::vector<hipModule_t> modules;
+};
+
+class Jit {
+ public:
+  ~Jit() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (worker_.joinable()) worker_.join();
+  }
+
+  // The entry for key, created and queued for compilation if new (nullptr
+  // when the kernel budget is spent). In Sync mode waits for the compile.
+  std::shared_ptr<Entry> get(const std::string &key, const std::string &src) {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = entries_.find(key);
+    std::shared_ptr<Entry> e;
+    if (it != entries_.end()) {
+      e = it->second;
+    } else {
+      if (entries_.size() >= max_kernels()) return nullptr;
+      e = std::make_shared<Entry>();
+      e->src = src;
+      entries_.emplace(key, e);
+      queue_.push_back(e);
+      pending_++;
+      if (!worker_.joinable()) worker_ = std::thread([this] { run(); });
+      cv_.notify_all();
+    }
+    if (mode() == Mode::Sync) cv_.wait(lk, [&] { return e->state != Entry::Pending; });
+    return e;
+  }
+
+  // Device function of a ready entry (module loaded on first use per device;
+  // the caller has made `device` current).
+  hipError_t function(Entry &e, int device, hipFunction_t *f) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = e.fn.find(device);
+    if (it != e.fn.end()) {
+      *f = it->second;
+      return hipSuccess;
+    }
+    hipModule_t m = nullptr;
+    hipError_t r = hipModuleLoadData(&m, e.code.data());
+    if (r != hipSuccess) return r;
+    r = hipModuleGetFunction(f, m, "storb_bs_jit");
+    if (r != hipSuccess) return r;
+    e.modules.push_back(m);
+    e.fn[device] = *f;
+    return hipSuccess;
+  }
+
+  void wait_for(const Entry &e) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return e.state != Entry::Pending; });
+  }
+
+  void wait_idle() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+  void stats(storb_rs_jit_stats_t *s) {
+    std::lock_guard<std::mutex> lk(mu_);
+    s->compiled = compiled_;
+    s->failed = failed_;
+    s->pending = pending_;
+    s->launches = launches;
+    s->fallbacks = fallbacks;
+    s->compile_ms = compile_ms_;
+  }
+
+  std::atomic<uint64_t> launches{0}, fallbacks{0};
+
+ private:
+  void run() {
+    for (;;) {
+      std::shared_ptr<Entry> e;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+        if (stop_) return;
+        e = queue_.front();
+        queue_.pop_front();
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      std::vector<char> code;
+      std::string log;
+      const bool ok = compile(e->src, code, log);
+      const double ms =
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        e->code = std::move(code);
+        e->log = std::move(log);
+        e->state = ok ? Entry::Ready : Entry::Failed;
+        (ok ? compiled_ : failed_)++;
+        compile_ms_ += ms;
+        pending_--;
+      }
+      if (!ok && std::getenv("STORB_RS_JIT_VERBOSE"))
+        std::fprintf(stderr, "storb_rs jit: compile failed:\n%s\n", e->log.c_str());
+      if (const char *dir = std::getenv("STORB_RS_JIT_DUMP")) {  // inspect with hipcc -S
+        const std::string path = std::string(dir) + "/storb_bs_jit_" +
+                                 std::to_string(compiled_ + failed_) + ".hip";
+        if (FILE *f = std::fopen(path.c_str(), "w")) {
+          std::fputs(e->src.c_str(), f);
+          std::fclose(f);
+        }
+      }
+      cv_.notify_all();
+    }
+  }
+
+  static bool compile(const std::string &src, std::vector<char> &code, std::string &log) {
+    hiprtcProgram prog = nullptr;
+    const char *hdrs[] = {kRsArgsH, kRsBitsliceCoreH};
+    const char *names[] = {"rs_args.h", "rs_bitslice_core.h"};
+    if (hiprtcCreateProgram(&prog, src.c_str(), "storb_bs_jit.hip", 2, hdrs, names) !=
+        HIPRTC_SUCCESS)
+      return false;
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    size_t n = 0;
+    if (hiprtcGetProgramLogSize(prog, &n) == HIPRTC_SUCCESS && n > 1) {
+      log.resize(n);
+      hiprtcGetProgramLog(prog, &log[0]);
+    }
+    bool ok = r == HIPRTC_SUCCESS && hiprtcGetCodeSize(prog, &n) == HIPRTC_SUCCESS && n > 0;
+    if (ok) {
+      code.resize(n);
+      ok = hiprtcGetCode(prog, code.data()) == HIPRTC_SUCCESS;
+    }
+    hiprtcDestroyProgram(&prog);
+    return ok;
+  }
+
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<std::string, std::shared_ptr<Entry>> entries_;
+  std::deque<std::shared_ptr<Entry>> queue_;
+  std::thread worker_;
+  bool stop_ = false;
+  uint64_t compiled_ = 0, failed_ = 0, pending_ = 0;
+  double compile_ms_ = 0;
+};
+
+Jit &jit() {
+  static Jit j;
+  return j;
+}
+
+// Resident workgroups per CU (the LDS reservation of rs_kernels.hpp cap_lds,
+// baked into the kernel as static LDS): the bit-sliced encoder's tuning,
+// 2 at k = 16, uncapped at k = 32 (profiles/r1_occupancy.txt).
+int occ_cap(uint32_t k) { return wg_cap(k == 16 ? 2 : 0); }
+
+// The kernel source for a (rows x k) matrix: bit b' of row[p][j][b] is bit b
+// of coef[p][j] * 2^b' (the GF(2) matrix of multiplication by coef[p][j]).
+std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask,
+                   int group, size_t lds) {
+  const GF256 &g = gf();
+  std::string s;
+  s.reserve(64 + static_cast<size_t>(rows) * k * 40);
+  s += "#include \"rs_bitslice_core.h\"\nnamespace {\nstruct JitMat {\n";
+  s += "  static constexpr int K = " + std::to_string(k) + ", R = " + std::to_string(rows) + ";\n";
+  s += "  static constexpr unsigned long long copy_mask = " + std::to_string(copy_mask) + "ull;\n";
+  s += "  struct Net { unsigned char row[R][K][8]; };\n  static constexpr Net net = {{";
+  for (uint32_t p = 0; p < rows; p++) {
+    s += p ? ",{" : "{";
+    for (uint32_t j = 0; j < k; j++) {
+      const uint8_t c = coef[static_cast<size_t>(p) * k + j];
+      s += j ? ",{" : "{";
+      for (int b = 0; b < 8; b++) {
+        unsigned m = 0;
+        for (int bp = 0; bp < 8; bp++)
+          if ((g.mul(c, static_cast<uint8_t>(1u << bp)) >> b) & 1u) m |= 1u << bp;
+        if (b) s += ',';
+        s += std::to_string(m);
+      }
+      s += '}';
+    }
+    s += '}';
+  }
+  s += "}};\n};\n}  // namespace\n";
+  s += "extern \"C\" __global__ __launch_bounds__(256) void storb_bs_jit(const "
+       "storb_rs::ApplyArgs a) {\n";
+  if (lds >= 4) {
+    // Static LDS reserving 160 KiB / cap per workgroup (occupancy cap).
+    s += "  __shared__ unsigned occ_pad[" + std::to_string(lds / 4) + "];\n";
+    s += "  asm volatile(\"\" :: \"s\"(occ_pad));  // keeps the unused array allocated\n";
+  }
+  s += "  storb_rs::bs::bs_kernel_body<JitMat, " + std::to_string(group) + ">(a);\n}\n";
+  return s;
+}
+
+}  // namespace
+
+bool enabled() { return mode() != Mode::Off; }
+
+// Worth a compiled kernel when the table kernel would be VALU-bound: its
+// ~5.6 VALU per (input, output, dword) plus ~5 selector ops per input
+// dword, over 4(k + r) bytes moved per dword column, above ~4.2 ops per
+// byte (the HBM-rate VALU budget measured in profiles/r1_valu_rate.txt is
+// ~5.2). RS(16, r >= 3), RS(32, r >= 3), RS(8, r >= 4); only for batches
+// large enough to matter.
+static bool valu_bound(uint32_t k, uint32_t rows) {
+  if (k < 8 || k > static_cast<uint32_t>(kSlotK) || rows == 0 ||
+      rows > static_cast<uint32_t>(kSlotR))
+    return false;
+  const double ops = 5.6 * k * rows + 5.0 * k;
+  return ops / (4.0 * (k + rows)) > 4.2;
+}
+
+bool wanted(uint32_t k, uint32_t rows, uint64_t bytes) {
+  return enabled() && bytes >= (4ull << 20) && valu_bound(k, rows);
+}
+
+// The cache entry of a (k x r) matrix with the given copy mask: looked up,
+// or created and queued. wait: block until its compile has finished.
+static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *coef,
+                                        uint64_t copy_mask, bool wait) {
+  const int group = bs::bs_group(static_cast<int>(k), static_cast<int>(r));
+  const size_t lds = cap_lds(occ_cap(k), 0);
+  std::string key(24 + static_cast<size_t>(r) * k, '\0');
+  const uint64_t hdr[3] = {(static_cast<uint64_t>(k) << 32) | r, copy_mask,
+                           (static_cast<uint64_t>(group) << 32) | lds};
+  std::memcpy(&key[0], hdr, sizeof(hdr));
+  std::memcpy(&key[24], coef, static_cast<size_t>(r) * k);
+  Jit &J = jit();
+  auto e = J.get(key, source(k, r, coef, copy_mask, group, lds));
+  if (e && wait) J.wait_for(*e);
+  return e;
+}
+
+hipError_t try_launch(int device, const ApplyArgs &a, const uint8_t *coef, hipStream_t s,
+                      bool *launched) {
+  *launched = false;
+  if (a.k == 0 || a.k > static_cast<uint32_t>(kSlotK) || a.r == 0 ||
+      a.r > static_cast<uint32_t>(kSlotR) || a.accumulate || !vector_ok(a))
+    return hipSuccess;
+  const uint64_t cols = a.block >> 4;
+  const uint64_t blocks = ((cols + bs::kBsColsPerTile - 1) / bs::kBsColsPerTile) * a.nstripes;
+  if (blocks == 0 || blocks > 0x7FFFFFFFull) return hipSuccess;  // table kernel handles it
+  uint64_t copy_mask = 0;
+  for (uint32_t j = 0; a.ncopy && j < a.k; j++)
+    if (a.copy[j]) copy_mask |= 1ull << j;
+  Jit &J = jit();
+  auto e = entry_for(a.k, a.r, coef, copy_mask, false);
+  if (!e || e->state != Entry::Ready) {
+    J.fallbacks++;
+    return hipSuccess;
+  }
+  hipFunction_t f = nullptr;
+  hipError_t r = J.function(*e, device, &f);
+  if (r != hipSuccess) return r;
+  ApplyArgs arg = a;
+  void *params[] = {&arg};
+  r = hipModuleLaunchKernel(f, static_cast<unsigned>(blocks), 1, 1, bs::kBsThreads, 1, 1, 0, s,
+                            params, nullptr);
+  if (r != hipSuccess) return r;
+  J.launches++;
+  *launched = true;
+  return hipSuccess;
+}
+
+int prepare(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask, bool wait) {
+  if (!enabled() || !valu_bound(k, rows)) return 0;
+  auto e = entry_for(k, rows, coef, copy_mask, wait);
+  if (!e) return 0;
+  return e->state == Entry::Ready ? 1 : (e->state == Entry::Failed ? -1 : 0);
+}
+
+}  // namespace jit
+}  // namespace storb_rs
+
+extern "C" {
+
+int storb_rs_jit_wait(void) {
+  storb_rs::jit::jit().wait_idle();
+  return STORB_RS_OK;
+}
+
+int storb_rs_jit_stats(storb_rs_jit_stats_t *out) {
+  if (!out) return STORB_RS_EINVAL;
+  storb_rs::jit::jit().stats(out);
+  return STORB_RS_OK;
+}
+
+}  // extern "C"

@@ -10,6 +10,7 @@
 #include <cstdint>
 
 #include "gf256.hpp"
+#include "rs_args.h"
 
 // Store policy of the shard kernels (rs_device.hpp, rs_bitslice.hpp): 1 =
 // non-temporal stores (measured fastest in steady state), 0 = default
@@ -20,35 +21,7 @@
 
 namespace storb_rs {
 
-// One launch applies a (r x k) coefficient block to k input share slots and
-// writes (or XOR-accumulates into) r output share slots, for every stripe.
-// Larger matrices are tiled over several launches by the host (apply.cpp).
-constexpr int kSlotK = 32;
-constexpr int kSlotR = 16;
-
-struct ApplyArgs {
-  const uint8_t *in[kSlotK];
-  uint64_t in_stride[kSlotK];
-  uint8_t *out[kSlotR];
-  uint64_t out_stride[kSlotR];
-  const PermTab *ptab;  // nibble tables [col][tab_rows], rows >= r zeroed
-  const uint8_t *btab;  // 256-byte product tables, same order (LDS variant)
-  uint32_t k, r;
-  uint32_t tab_rows;    // row stride of both tables = rows_bucket(r)
-  uint64_t block;       // bytes per share
-  uint32_t nstripes;
-  uint32_t accumulate;  // 1: out ^= result (column tiling), 0: out = result
-  // Fused assembly (decode into a separate chunk buffer): input slot j is
-  // also stored, as loaded, to copy[j] (null = not copied). ncopy > 0 selects
-  // the COPY kernels (KM <= kCopyMaxK); r may then be 0 (pure assembly).
-  uint32_t ncopy;
-  uint8_t *copy[kSlotK];
-  uint64_t copy_stride[kSlotK];
-};
-
-// Largest k bucket with COPY instantiations; wider decodes copy survivors
-// with hipMemcpy2DAsync before the kernel.
-constexpr uint32_t kCopyMaxK = 16;
+// ApplyArgs, kSlotK / kSlotR, kCopyMaxK: rs_args.h (shared with the JIT).
 
 enum class Variant { Perm = 1, Lds = 2 };
 

@@ -27,6 +27,7 @@
 
 #include "blake3.hpp"
 #include "ctx.hpp"
+#include "rs_jit.hpp"
 
 using namespace storb_rs;
 using namespace storb_rs::detail;
@@ -183,18 +184,91 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
   return STORB_RS_OK;
 }
 
-// out_r = sum_j coef[r][j] * in_j for all stripes, tiled into slot blocks.
-// copy (optional, fused assembly): copy[j] != null stores input j there as
-// it is loaded (copy_fusable() must hold); rows may then be 0.
+// STORB_RS_FUSED_ASSEMBLY=0: survivors are copied before the kernel instead
+// of by it (kept for the A/B measurement).
+static bool fused_assembly_on() {
+  const char *e = std::getenv("STORB_RS_FUSED_ASSEMBLY");
+  return e == nullptr || e[0] != '0';
+}
+
+// Whether the table kernel's COPY instantiations can do the assembly: they
+// exist for k <= kCopyMaxK in the dwordx4 register-table kernel (not the LDS
+// comparison variant), and every share base / stride must be 16-B aligned.
+static bool copy_fusable_table(const storb_rs_ctx *ctx, uint32_t k, size_t block,
+                               const uint8_t *const *d_in, const size_t *in_stride,
+                               uint8_t *const *copy, const size_t *copy_stride) {
+  if (k > kCopyMaxK || pick_variant(ctx) != Variant::Perm || block % 16) return false;
+  for (uint32_t j = 0; j < k; j++) {
+    if ((reinterpret_cast<uintptr_t>(d_in[j]) | in_stride[j]) % 16) return false;
+    if (copy[j] && (reinterpret_cast<uintptr_t>(copy[j]) | copy_stride[j]) % 16) return false;
+  }
+  return true;
+}
+
+static int copy_first(storb_rs_ctx *ctx, uint32_t k, const uint8_t *const *d_in,
+                      const size_t *in_stride, uint8_t *const *copy, const size_t *copy_stride,
+                      size_t block, uint32_t nstripes, hipStream_t s) {
+  for (uint32_t j = 0; j < k; j++)
+    if (copy[j])
+      HIP_TRY(ctx, hipMemcpy2DAsync(copy[j], copy_stride[j], d_in[j], in_stride[j], block, nstripes,
+                                    hipMemcpyDeviceToDevice, s));
+  return STORB_RS_OK;
+}
+
+// out_r = sum_j coef[r][j] * in_j for all stripes. copy (optional, decode
+// into a separate chunk buffer): copy[j] != null receives input j as well;
+// rows may then be 0 (pure assembly).
+//
+// Kernel choice: under AUTO a matrix the table kernel would be VALU-bound on
+// runs its own compiled bit-sliced kernel once that is built (rs_jit.cpp;
+// assembly fused for any k <= 32); otherwise the table kernel, tiled into
+// kSlotR x kSlotK blocks, with the assembly fused for k <= kCopyMaxK and
+// done by copies first above that.
 int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
           const uint8_t *const *d_in, const size_t *in_stride, uint8_t *const *d_out,
           const size_t *out_stride, size_t block, uint32_t nstripes, hipStream_t s,
           uint8_t *const *copy, const size_t *copy_stride) {
   if ((rows == 0 && !copy) || block == 0 || nstripes == 0) return STORB_RS_OK;
+  int rc;
+  if (copy && !fused_assembly_on()) {
+    if ((rc = copy_first(ctx, k, d_in, in_stride, copy, copy_stride, block, nstripes, s))) return rc;
+    copy = nullptr;
+    if (rows == 0) return STORB_RS_OK;
+  }
+  if (rows > 0 && ctx->variant == STORB_RS_KERNEL_AUTO && k <= static_cast<uint32_t>(kSlotK) &&
+      rows <= static_cast<uint32_t>(kSlotR) &&
+      jit::wanted(k, rows, static_cast<uint64_t>(k + rows) * block * nstripes)) {
+    ApplyArgs a{};
+    a.k = k;
+    a.r = rows;
+    for (uint32_t j = 0; j < k; j++) {
+      a.in[j] = d_in[j];
+      a.in_stride[j] = in_stride[j];
+      if (copy && copy[j]) {
+        a.copy[j] = copy[j];
+        a.copy_stride[j] = copy_stride[j];
+        a.ncopy++;
+      }
+    }
+    for (uint32_t i = 0; i < rows; i++) {
+      a.out[i] = d_out[i];
+      a.out_stride[i] = out_stride[i];
+    }
+    a.block = block;
+    a.nstripes = nstripes;
+    bool launched = false;
+    HIP_TRY(ctx, jit::try_launch(ctx->device, a, coef, s, &launched));
+    if (launched) return STORB_RS_OK;
+  }
+  if (copy && !copy_fusable_table(ctx, k, block, d_in, in_stride, copy, copy_stride)) {
+    if ((rc = copy_first(ctx, k, d_in, in_stride, copy, copy_stride, block, nstripes, s))) return rc;
+    copy = nullptr;
+    if (rows == 0) return STORB_RS_OK;
+  }
   Tables *t = nullptr;
   const std::vector<uint8_t> zero_row(k, 0);
   const uint32_t trows = rows ? rows : 1;  // pure assembly: one zero row of tables
-  int rc = get_tables(ctx, k, trows, rows ? coef : zero_row.data(), s, &t);
+  rc = get_tables(ctx, k, trows, rows ? coef : zero_row.data(), s, &t);
   if (rc) return rc;
   const Variant v = pick_variant(ctx);
   size_t bi = 0;
@@ -229,23 +303,6 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
       }
     }
   return tables_used(ctx, t, s);
-}
-
-// Whether a decode into a separate buffer can assemble the chunk inside the
-// kernel: the COPY instantiations exist for k <= kCopyMaxK in the dwordx4
-// register-table kernel (not the LDS comparison variant), and every share
-// base / stride must be 16-B aligned.
-bool copy_fusable(const storb_rs_ctx *ctx, uint32_t k, size_t block,
-                  const uint8_t *const *d_in, const size_t *in_stride, size_t out_stride,
-                  const uint8_t *d_out) {
-  if (k > kCopyMaxK || pick_variant(ctx) != Variant::Perm || block % 16 ||
-      out_stride % 16 || reinterpret_cast<uintptr_t>(d_out) % 16)
-    return false;
-  for (uint32_t j = 0; j < k; j++)
-    if ((reinterpret_cast<uintptr_t>(d_in[j]) | in_stride[j]) % 16) return false;
-  // STORB_RS_FUSED_ASSEMBLY=0: copy first (kept for the A/B measurement)
-  return std::getenv("STORB_RS_FUSED_ASSEMBLY") == nullptr ||
-         std::getenv("STORB_RS_FUSED_ASSEMBLY")[0] != '0';
 }
 
 // Parity of (k, n) = enc[k..n) * data. Under the AUTO variant the geometries
@@ -674,23 +731,16 @@ int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t 
     out[r] = d_out + static_cast<size_t>(missing[r]) * block;
   // Surviving data shares: in place when d_out aliases d_data; else stored
   // to their slots of d_out by the decode kernel itself as it reads them
-  // (fused assembly), or, where that kernel does not apply, copied first.
-  if (d_out != d_data || out_stride != data_stride) {
-    std::vector<uint8_t *> copy(k, nullptr);
-    std::vector<size_t> copys(k, out_stride);
+  // (fused assembly), or, where no such kernel applies, copied first (apply).
+  std::vector<uint8_t *> copy(k, nullptr);
+  std::vector<size_t> copys(k, out_stride);
+  const bool assemble = d_out != d_data || out_stride != data_stride;
+  if (assemble)
     for (uint32_t c = 0; c < k; c++)
       if (slot_idx[c] < k) copy[c] = d_out + static_cast<size_t>(c) * block;
-    if (copy_fusable(ctx, k, block, in.data(), ins.data(), out_stride, d_out))
-      return apply(ctx, k, static_cast<uint32_t>(missing.size()), coef.data(), in.data(),
-                   ins.data(), out.data(), outs.data(), block, nstripes, s, copy.data(),
-                   copys.data());
-    for (uint32_t c = 0; c < k; c++)
-      if (copy[c])
-        HIP_TRY(ctx, hipMemcpy2DAsync(copy[c], out_stride, in[c], ins[c], block, nstripes,
-                                      hipMemcpyDeviceToDevice, s));
-  }
-  return apply(ctx, k, static_cast<uint32_t>(missing.size()), coef.data(), in.data(),
-               ins.data(), out.data(), outs.data(), block, nstripes, s);
+  return apply(ctx, k, static_cast<uint32_t>(missing.size()), coef.data(), in.data(), ins.data(),
+               out.data(), outs.data(), block, nstripes, s, assemble ? copy.data() : nullptr,
+               assemble ? copys.data() : nullptr);
 }
 
 int storb_rs_repair_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
@@ -735,6 +785,23 @@ int storb_rs_repair_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t 
   DeviceGuard g(ctx->device);
   return apply(ctx, k, ntargets, coef.data(), in.data(), ins.data(), out.data(), outs.data(),
                block, nstripes, pick_stream(ctx, hip_stream));
+}
+
+int storb_rs_jit_prepare_decode(uint32_t k, uint32_t n, const uint32_t *share_idx,
+                                uint32_t nshares, int assemble, int wait) {
+  if (!valid_params(k, n) || !share_idx) return STORB_RS_EINVAL;
+  std::vector<uint32_t> slot_idx, slot_pos, missing;
+  int rc = select_shares(nullptr, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint8_t> coef;
+  rc = decode_rows(nullptr, k, n, slot_idx, coef, missing);
+  if (rc || missing.empty()) return rc;
+  uint64_t mask = 0;
+  for (uint32_t c = 0; assemble && c < k && c < 64; c++)
+    if (slot_idx[c] < k) mask |= 1ull << c;
+  return jit::prepare(k, static_cast<uint32_t>(missing.size()), coef.data(), mask, wait != 0) < 0
+             ? STORB_RS_EDEVICE
+             : STORB_RS_OK;
 }
 
 // Host BLAKE3 (blake3_host.cpp: 16 chunks per AVX-512 compression where

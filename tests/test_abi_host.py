@@ -101,3 +101,25 @@ def test_no_device_is_an_error_not_a_fallback():
     with pytest.raises(_lib.StorbRsError) as e:
         _lib.Context(-1)
     assert e.value.code == _lib.ENODEV
+
+
+def test_jit_compiles_decode_kernels_without_gpu():
+    """The run-time-compiled decode kernels build with hipRTC on the host
+    (no GPU): RS(16,8) with every data share lost, in place and assembled,
+    and RS(32,16) with 16 lost. Matrices the policy does not want (RS(4,2),
+    RS(8,4) with 3 lost) queue nothing."""
+    from storb_amd import _lib
+    before = _lib.jit_stats()
+    _lib.jit_prepare_decode(4, 6, [2, 3, 4, 5])
+    _lib.jit_prepare_decode(8, 12, [1, 2, 4, 6, 7, 8, 9, 10, 11])
+    assert _lib.jit_stats()["compiled"] == before["compiled"]
+    _lib.jit_prepare_decode(16, 24, list(range(8, 24)))
+    _lib.jit_prepare_decode(16, 24, [1, 2, 3, 5, 8, 13, 16, 17, 18, 19, 20, 21, 22, 23, 4, 6],
+                            assemble=True)
+    _lib.jit_prepare_decode(32, 48, list(range(16, 48)))
+    st = _lib.jit_stats()
+    assert st["failed"] == 0 and st["pending"] == 0
+    assert st["compiled"] == before["compiled"] + 3
+    # the same pattern again is a cache hit
+    _lib.jit_prepare_decode(16, 24, list(range(8, 24)))
+    assert _lib.jit_stats()["compiled"] == st["compiled"]
