@@ -74,6 +74,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--no-check", action="store_true")
+    p.add_argument("--no-traffic", action="store_true",
+                   help="skip the live HBM-traffic passes (rocprofv3 --pmc FETCH_SIZE / "
+                        "WRITE_SIZE on a short child run of the same workload)")
+    p.add_argument("--minimal", action="store_true",
+                   help="the timed line only (no traffic passes, copy ceiling, CPU baseline, "
+                        "host path, hashing, repair); used for the traffic child runs")
     p.add_argument("--no-host-path", action="store_true")
     p.add_argument("--leg-events", choices=["each", "ends"], default="ends",
                    help="ends: HIP events only around the timed region, per-leg times "
@@ -413,6 +419,86 @@ def config4_storb_faithful(ctx, w, stream, reps=5):
                     "chunks, k=2, m=3, one batched launch; bytes = k*B read + (n-k)*B written"}
 
 
+def leg_kernel_match(a, w, leg):
+    """Substring of the rocprofv3 kernel name each leg launches."""
+    if leg == "encode":
+        if a.kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48)):
+            return f"rs_encode_bitslice<{w.k}, {w.n}>"
+        k, r = w.k, w.n - w.k
+    else:
+        if w.jit_decode:
+            return "storb_bs_jit"
+        k, r = w.k, sum(1 for x in w.erased if x < w.k)
+    kb = 1
+    while kb < min(k, 32):
+        kb <<= 1
+    return f"rs_apply_{'lds' if a.kernel == 'lds' else 'perm'}<{kb}, {r if r <= 8 else 16},"
+
+
+def pmc_traffic(a, w):
+    """HBM bytes per launch measured in THIS run (roofline.traffic): two short
+    child runs of the same workload under rocprofv3, one per counter
+    (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), each under a hard
+    time limit. gfx950 correction (MI355X_MICROARCH.md, HBM): read bytes =
+    2 x FETCH_SIZE KiB for 16-B-per-lane streaming loads; WRITE_SIZE is exact
+    for 16-B-per-lane stores. Per leg: median over that kernel's launches."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return {"traffic": None, "traffic_source": "rocprofv3 not found"}
+    child = [sys.executable, os.path.abspath(__file__), "--config", str(a.config),
+             "--steps", "3", "--warmup", "1", "--minimal", "--no-check", "--kernel", a.kernel,
+             "--objects", str(a.objects)]
+    if a.chunks:
+        child += ["--chunks", str(a.chunks)]
+    if a.erase is not None:
+        child += ["--erase", str(a.erase)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    t0 = time.perf_counter()
+    for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="storb_pmc_", dir="/tmp")
+        try:
+            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", cnt, "--kernel-trace",
+                   "--output-format", "csv", "-d", d, "-o", "run", "--", *child]
+            r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, text=True)
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                return {"traffic": None,
+                        "traffic_source": f"rocprofv3 --pmc {cnt} failed (rc {r.returncode}): "
+                                          f"{r.stderr.strip()[-300:]}"}
+            for row in csv.DictReader(open(files[0])):
+                if row["Counter_Name"] == cnt:
+                    vals.setdefault((row["Kernel_Name"], cnt), []).append(
+                        float(row["Counter_Value"]))
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    by_leg = {}
+    for leg in w.legs:
+        sub = leg_kernel_match(a, w, leg)
+        f = [v for (kn, c), xs in vals.items() if c == "FETCH_SIZE" and sub in kn for v in xs]
+        wr = [v for (kn, c), xs in vals.items() if c == "WRITE_SIZE" and sub in kn for v in xs]
+        if not f or not wr:
+            return {"traffic": None, "traffic_source": f"no {sub} launches in the PMC passes"}
+        fk, wk = statistics.median(f), statistics.median(wr)
+        b = 2 * fk * 1024 + wk * 1024
+        by_leg[leg] = {"kernel": sub, "launches": len(f), "FETCH_SIZE_KiB": fk,
+                       "WRITE_SIZE_KiB": wk, "bytes": b,
+                       "vs_algorithmic": round(b / w.alg_bytes(leg), 5)}
+    first = by_leg[w.legs[0]]
+    return {"traffic": first["bytes"], "traffic_by_leg": by_leg,
+            "traffic_source": (f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a "
+                               f"3-step child run of this workload ({time.perf_counter() - t0:.0f}"
+                               f" s); read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE")}
+
+
 def kernel_names(kernel, w):
     """The kernels the legs launch (rs_bitslice.hpp / rs_device.hpp)."""
     names = {}
@@ -666,18 +752,6 @@ def main():
     # also bytes per launch / average launch duration)
     achieved = sum(alg.values()) / (gpu_ms * 1e-3) / 1e9
 
-    traffic = None
-    tpath = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if a.config == 2 and os.path.exists(tpath):
-        try:
-            t = json.load(open(tpath))
-            if (t.get("kernel") in (a.kernel, "perm" if a.kernel == "auto" else None)
-                    and t.get("chunks") == w.N
-                    and t.get("chunk_bytes") == w.chunk):
-                traffic = t.get("bytes_per_launch")
-        except Exception:
-            traffic = None
-
     out = {
         "metric": w.metric,
         "value": round(value, 3),
@@ -706,7 +780,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
+            "traffic": None,
+            "traffic_source": "not measured (N > 1, --minimal or --no-traffic)",
             "kernel": kernel_names(a.kernel, w),
             "gpu_ms_per_step": round(gpu_ms, 4),
             "launch_ms": round(gpu_ms / len(legs), 4),
@@ -721,7 +796,10 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not a.minimal:
+        if not a.no_traffic:
+            pmc = pmc_traffic(a, w)
+            out["roofline"].update(pmc)
         out["roofline"]["copy_ceiling_gbs"] = copy_ceiling(ctx, dev, stream)
         if a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.erased), a.cpu_seconds,

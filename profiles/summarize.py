@@ -1,81 +1,85 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 CSV output into the committed per-round summaries.
+"""Turn a round's GPU-box profile directory (tools/profile_round.sh) into the
+committed summaries under profiles/.
 
-usage: summarize.py ROUND TRACE_DIR FETCH_DIR WRITE_DIR [--kernel SUBSTR]
+usage: summarize.py ROUND PROF_DIR
 
-* copies the --kernel-trace --stats summary to profiles/ROUND_kernel_stats.csv
-* reduces the two PMC passes (FETCH_SIZE, WRITE_SIZE -- separate passes, the
-  TCC block cannot hold both) to per-launch HBM bytes for the hot kernel and
-  writes profiles/ROUND_pmc.json and profiles/pmc_traffic.json (read by
-  bench.py for roofline.traffic).
-
-gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports
-exactly half the bytes of a wide coalesced streaming read (16 B/lane
-dwordx4), so read bytes = 2 * FETCH_SIZE KiB; WRITE_SIZE is exact for
-16-B-per-lane streaming stores. Both counters are in KiB.
+For every PROF_DIR/trace_<name>/ (rocprofv3 --kernel-trace --stats of one
+bench.py run):
+  * profiles/<ROUND>_<name>_kernel_stats.csv  -- the --stats summary as is
+  * profiles/<ROUND>_bench_<name>.json       -- that run's bench line
+and a check that each leg's kernel average duration from the trace agrees
+with the bench line's per-leg time (roofline.leg_ms, HIP events).
+PROF_DIR/bench_default.log (the untraced default run, whose
+roofline.traffic is measured live by its own FETCH_SIZE / WRITE_SIZE passes)
+becomes profiles/<ROUND>_bench.json. Prints a JSON summary.
 """
 import csv
 import glob
 import json
 import os
 import shutil
-import statistics
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def one(d, pat):
-    m = glob.glob(os.path.join(d, "**", pat), recursive=True)
-    if not m:
-        raise SystemExit(f"no {pat} under {d}")
-    return m[0]
+def last_json(path):
+    for line in reversed(open(path).read().strip().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise SystemExit(f"no JSON line in {path}")
 
 
-def counter(d, name, ksub):
-    rows = [r for r in csv.DictReader(open(one(d, "*counter_collection.csv")))
-            if ksub in r["Kernel_Name"] and r["Counter_Name"] == name]
-    return [float(r["Counter_Value"]) for r in rows], rows
+def kernel_match(line, leg):
+    """The rocprof name substring of the kernel a bench leg launched."""
+    byleg = line["roofline"].get("traffic_by_leg") or {}
+    if leg in byleg:
+        return byleg[leg]["kernel"]
+    name = line["roofline"]["kernel"][leg]
+    if name.startswith("storb_bs_jit"):
+        return "storb_bs_jit"
+    base, args = name.split("<", 1)
+    return f"{base}<{args.rstrip('>').replace(',', ', ')}"
 
 
 def main():
-    rnd, tdir, fdir, wdir = sys.argv[1:5]
-    ksub = "rs_apply_perm<4, 2, true>"
-    if "--kernel" in sys.argv:
-        ksub = sys.argv[sys.argv.index("--kernel") + 1]
-    stats = one(tdir, "*kernel_stats.csv")
-    shutil.copy(stats, os.path.join(HERE, f"{rnd}_kernel_stats.csv"))
-    avg_ns = None
-    for r in csv.DictReader(open(stats)):
-        if ksub in r["Name"]:
-            avg_ns = float(r["AverageNs"])
-    fetch, frows = counter(fdir, "FETCH_SIZE", ksub)
-    write, _ = counter(wdir, "WRITE_SIZE", ksub)
-    f_kib, w_kib = statistics.median(fetch), statistics.median(write)
-    read_b = 2 * f_kib * 1024
-    write_b = w_kib * 1024
-    out = {
-        "round": rnd,
-        "kernel": "perm",
-        "kernel_name": ksub,
-        "chunks": 1024,
-        "chunk_bytes": 1 << 20,
-        "launches_counted": len(fetch),
-        "FETCH_SIZE_KiB_median": f_kib,
-        "WRITE_SIZE_KiB_median": w_kib,
-        "read_bytes_per_launch": read_b,
-        "write_bytes_per_launch": write_b,
-        "bytes_per_launch": read_b + write_b,
-        "correction": "read = 2 x FETCH_SIZE (gfx950 half-count on dwordx4 streams)",
-        "avg_kernel_ns_from_trace": avg_ns,
-        "vgpr": frows[0]["VGPR_Count"] if frows else None,
-        "sgpr": frows[0]["SGPR_Count"] if frows else None,
-    }
-    if avg_ns:
-        out["achieved_GBps_from_trace"] = round((read_b + write_b) / avg_ns, 1)
-    json.dump(out, open(os.path.join(HERE, f"{rnd}_pmc.json"), "w"), indent=1)
-    json.dump(out, open(os.path.join(HERE, "pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1))
+    rnd, pdir = sys.argv[1:3]
+    summary = {}
+    for tdir in sorted(glob.glob(os.path.join(pdir, "trace_*"))):
+        name = os.path.basename(tdir)[len("trace_"):]
+        stats = glob.glob(os.path.join(tdir, "**", "*kernel_stats.csv"), recursive=True)
+        if not stats:
+            continue
+        dst = os.path.join(HERE, f"{rnd}_{name}_kernel_stats.csv")
+        shutil.copy(stats[0], dst)
+        line = last_json(os.path.join(pdir, f"bench_{name}.log"))
+        json.dump(line, open(os.path.join(HERE, f"{rnd}_bench_{name}.json"), "w"))
+        rows = list(csv.DictReader(open(stats[0])))
+        legs = {}
+        for leg, ms in line["roofline"]["leg_ms"].items():
+            sub = kernel_match(line, leg)
+            hit = [r for r in rows if sub in r["Name"]]
+            if not hit:
+                legs[leg] = {"kernel": sub, "trace": None}
+                continue
+            r = max(hit, key=lambda x: int(x["Calls"]))
+            avg_ms = float(r["AverageNs"]) / 1e6
+            alg = line["roofline"]["alg_bytes_per_launch"][leg]
+            legs[leg] = {"kernel": r["Name"], "calls": int(r["Calls"]),
+                         "trace_avg_ms": round(avg_ms, 4), "bench_leg_ms": ms,
+                         "trace_GBps": round(alg / (avg_ms * 1e-3) / 1e9, 1),
+                         "trace_frac_of_8TBps": round(alg / (avg_ms * 1e-3) / 8e12, 4)}
+        summary[name] = {"value": line["value"], "frac": line["roofline"]["frac"], "legs": legs}
+    dflt = os.path.join(pdir, "bench_default.log")
+    if os.path.exists(dflt):
+        line = last_json(dflt)
+        json.dump(line, open(os.path.join(HERE, f"{rnd}_bench.json"), "w"))
+        summary["default"] = {"value": line["value"], "frac": line["roofline"]["frac"],
+                              "traffic": line["roofline"].get("traffic"),
+                              "traffic_source": line["roofline"].get("traffic_source")}
+    json.dump(summary, open(os.path.join(HERE, f"{rnd}_summary.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
 
 
 if __name__ == "__main__":

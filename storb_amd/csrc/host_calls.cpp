@@ -77,6 +77,15 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
   for (uint32_t i = 0; i < p; i++)
     if (!parity_out[i]) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
+  if (k == 1) {
+    // Storb sizes every chunk <= 64 KiB (objects < 256 KiB) k = 1, m = 2
+    // (piece.rs:307-317). Every generator row is then [1] -- a single data
+    // share's Vandermonde column is all ones -- so each parity share IS the
+    // data share: a copy with no GF(2^8) work to offload, where a device
+    // round trip would only add launch and PCIe latency.
+    for (uint32_t i = 0; i < p; i++) std::memcpy(parity_out[i], data, len);
+    return STORB_RS_OK;
+  }
   const size_t S = round_up(B, kAlign);
   const bool zc = static_cast<size_t>(n) * S <= ctx->zc_max;
   // Page-locked, 16-B aligned caller buffers need no staging at all.
@@ -188,6 +197,10 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
     put_present();
     return STORB_RS_OK;
   }
+  if (k == 1) {  // any share of a k = 1 code is the data (encode_one)
+    std::memcpy(out, shares[slot_pos[0]], outlen);
+    return STORB_RS_OK;
+  }
   const size_t S = round_up(block, kAlign);
   const uint32_t e = static_cast<uint32_t>(missing.size());
   const bool zc = static_cast<size_t>(k + e) * S <= ctx->zc_max;
@@ -293,6 +306,10 @@ static int repair_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   std::vector<uint8_t> coef;
   rc = repair_rows(ctx, k, n, slot_idx, targets, ntargets, coef);
   if (rc || ntargets == 0) return rc;
+  if (k == 1) {  // every share of a k = 1 code is the same bytes (encode_one)
+    for (uint32_t r = 0; r < ntargets; r++) std::memcpy(out[r], shares[slot_pos[0]], block);
+    return STORB_RS_OK;
+  }
   const size_t S = round_up(block, kAlign);
   DeviceGuard g(ctx->device);
   HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));

@@ -118,3 +118,44 @@ def test_loopback_roundtrip_small(gpus):
     assert res["ack_mismatch"] == 0
     assert res["chunks_decoded_through_parity"] > 0
     assert res["contexts"] == (gpus or max(1, res["visible_gpus"]))
+
+
+@pytest.mark.gpu
+def test_loopback_config5_geometry():
+    """BASELINE config 5 at its own geometry: a 640 MiB (+ tail) object cut by
+    Storb's own rule (upload.rs:209 piece_length) into 8 MiB chunks, each
+    k=16, m=24 (piece.rs:307-317), over 8 miners with one killed. Every piece
+    a miner stored and every piece id (computed on the GPU, and acked by the
+    miners over the store framing) is checked against the oracle's shares;
+    the host hasher used for that is pinned to the reference blake3
+    (test_blake3.py), which is also run itself on a sample of pieces."""
+    import loopback
+    from oracle import coracle
+    from storb_amd import _lib
+    size = (640 << 20) + 12345
+    seen = {}
+
+    def inspect(obj, metas, dirs):
+        geo = [(m["k"], m["m"], m["B"]) for m in metas]
+        assert geo.count((16, 24, 512 << 10)) == 80 and len(geo) == 81
+        for ci, meta in enumerate(metas):
+            chunk = obj[meta["off"]:meta["off"] + meta["len"]]
+            shares, B, pad = coracle.encode(meta["k"], meta["m"], chunk)
+            assert (B, pad) == (meta["B"], meta["padlen"])
+            for i in range(meta["m"]):
+                h = meta["hashes"][i]
+                assert h == _lib.blake3(shares[i]), (ci, i)
+                hx = h.hex()
+                with open(os.path.join(dirs[meta["miner"][i]], hx[:2], hx[2:]), "rb") as f:
+                    assert f.read() == shares[i].tobytes(), (ci, i)
+                if (ci, i) in ((0, 0), (0, 23), (40, 17)):
+                    assert ref(shares[i].tobytes()) == h, (ci, i)
+                    seen[(ci, i)] = True
+
+    res = loopback.run(argparse.Namespace(size=size, miners=8, seed=3, kill_seed=7, gpus=0,
+                                          cold=False), inspect=inspect)
+    assert len(seen) == 3
+    assert res["bit_exact"] and res["ack_mismatch"] == 0
+    assert [16, 24] in [list(x) for x in res["k_m"]] or (16, 24) in res["k_m"]
+    assert res["chunk_bytes"] == 8 << 20
+    assert res["chunks_decoded_through_parity"] > 0

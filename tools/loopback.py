@@ -123,7 +123,11 @@ def splitmix_bytes(seed: int, n: int) -> np.ndarray:
     return z.view(np.uint8)[:n]
 
 
-def run(a):
+def run(a, inspect=None):
+    """One loopback round trip; returns the JSON-able result. inspect (tests):
+    called as inspect(obj, metas, miner_dirs) before the miners' stores are
+    removed -- metas[c] holds chunk c's (k, m, B, padlen, off, len), its GPU
+    piece ids and the miner of every piece."""
     tmp = tempfile.mkdtemp(prefix="storb_loop_")
     miners = []
     for m in range(a.miners):
@@ -132,12 +136,13 @@ def run(a):
                                  "--store-port", str(sp), "--http-port", str(hp),
                                  "--dir", os.path.join(tmp, f"miner{m}")],
                                 stdout=subprocess.PIPE, text=True)
-        miners.append({"proc": proc, "store": sp, "http": hp})
+        miners.append({"proc": proc, "store": sp, "http": hp,
+                       "dir": os.path.join(tmp, f"miner{m}")})
     for m in miners:
         if m["proc"].stdout.readline().strip() != "ready":
             raise SystemExit("miner failed to start")
     try:
-        return _run(a, miners)
+        return _run(a, miners, inspect)
     finally:
         for m in miners:
             if m["proc"].poll() is None:
@@ -146,7 +151,7 @@ def run(a):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def _run(a, miners):
+def _run(a, miners, inspect=None):
     M = len(miners)
     # one context per GPU; chunks partition across them. With
     # more contexts than devices they share devices (multi-GPU rehearsal).
@@ -272,6 +277,8 @@ def _run(a, miners):
         "devices": [c.device for c in ctxs], "contexts": len(ctxs), "warm": not a.cold,
         "visible_gpus": _lib.device_count(),
     }
+    if inspect is not None:
+        inspect(obj, metas, [m["dir"] for m in miners])
     return res
 
 

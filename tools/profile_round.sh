@@ -1,28 +1,29 @@
 #!/bin/bash
-# Collects the round profiles on a GPU box into gpurun_out/prof_<ROUND>/:
-#   trace/  rocprofv3 --kernel-trace --stats of `python3 bench.py --no-host-path`
-#   fetch/, write/  separate FETCH_SIZE and WRITE_SIZE passes (TCC slots, MI355X_MICROARCH.md)
-#   bench_*.log  the bench lines (traced and untraced)
-# Then, back in the container:
-#   python3 profiles/summarize.py <ROUND> gpurun_out/prof_<ROUND>/{trace,fetch,write} --kernel ...
-# usage (via gpurun): bash tools/profile_round.sh r1
+# Collects a round's profiles on a GPU box into gpurun_out/prof_<ROUND>/:
+#   trace_<cfg>/   rocprofv3 --kernel-trace --stats of bench.py for each leg set
+#                  below (--no-host-path: the PCIe legs launch the same kernels
+#                  on host-staged batches and would blend into the averages)
+#   bench_<cfg>.log  the bench line of that traced run
+#   bench_default.log  the untraced default bench (the driver's command; its
+#                  roofline.traffic comes from its own live FETCH/WRITE passes)
+# Then, back in the container: python3 profiles/summarize.py <ROUND> gpurun_out/prof_<ROUND>
+# usage (via gpurun): bash tools/profile_round.sh r2
 set -euo pipefail
-ROUND=${1:-r1}
+ROUND=${1:-r2}
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/prof_$ROUND
 rm -rf "$OUT" && mkdir -p "$OUT"
-KSUB="rs_apply_perm<4, 2, 256, 1, false, 4, false, false, false>"
-# --no-host-path: the PCIe legs launch the same kernel on host-staged batches
-# (18 us .. 3.6 ms each), which would blend into its average; this run's own
-# bench line (bench_traced.log) is the one the stats are compared with.
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-  -- python3 bench.py --no-host-path > "$OUT/bench_traced.log" 2>&1
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" \
-  -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --no-host-path \
-  > "$OUT/fetch.log" 2>&1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" \
-  -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --no-host-path \
-  > "$OUT/write.log" 2>&1
-echo "$KSUB" > "$OUT/kernel.txt"
-timeout -k 10 300 python3 bench.py > "$OUT/bench_untraced.log" 2>&1
+trace() {  # name, bench args...
+  local name=$1
+  shift
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$name" \
+    -o run -- python3 bench.py --no-host-path --no-traffic --cpu-seconds 0 "$@" \
+    > "$OUT/bench_$name.log" 2>&1
+  echo "traced $name"
+}
+trace config2
+trace config5_erase8 --config 5 --erase 8
+trace config6_erase16 --config 6 --erase 16
+timeout -k 10 400 python3 bench.py > "$OUT/bench_default.log" 2>&1
+echo "default bench done"
 echo done
