@@ -273,3 +273,21 @@ def test_threaded_roundtrip_baseline_path():
     assert co.roundtrip_many(16, 24, data, 12345, 12, [0, 3, 5, 7, 9, 11, 13, 15], 3) == 0
     # losing more than n-k shares is a failure for every chunk
     assert co.roundtrip_many(4, 6, data, 12345, 12, [0, 1, 2], 2) == 12
+
+
+def test_named_assumption_fixtures(golden):
+    """Every behaviour pinned beyond fec.c (SURVEY 8(c) open item) is a named
+    fixture a networked session can confirm against zfec-rs in one run; the
+    oracle reproduces each, including the share order it is given."""
+    names = {v["name"] for v in golden["assumptions"]}
+    assert names == {"padlen_when_len_divisible_by_k", "padlen_when_len_not_divisible_by_k",
+                     "decode_of_unsorted_shares", "n_equals_k", "k_1_replication"}
+    for v in golden["assumptions"]:
+        k, n = v["k"], v["n"]
+        d = bytes.fromhex(v["data_hex"])
+        shares, B, pad = co.encode(k, n, d)
+        assert (B, pad) == (v["B"], v["padlen"]), v["name"]
+        assert [bytes(s).hex() for s in shares[k:]] == v.get("parity_hex", []), v["name"]
+        order = v["decode"].get("given_order", v["decode"].get("survivors"))
+        rec = co.decode(k, n, [shares[i] for i in order], order, B, pad)
+        assert sha(rec) == v["decode"]["data_sha256"] == sha(d), v["name"]

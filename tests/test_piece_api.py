@@ -126,6 +126,29 @@ def test_reference_inputs_match_golden_parity():
         assert [hashlib.sha256(p).hexdigest() for p in parity] == v["parity_sha256"], name
 
 
+@pytest.mark.gpu
+def test_assumption_fixtures_on_the_gpu_path():
+    """The named fixtures for behaviour beyond fec.c (padlen, unsorted shares,
+    n = k, k = 1) through the C ABI: parity bytes and decodes as pinned."""
+    from storb_amd import _lib
+    g = json.load(open(GOLDEN))
+    ctx = _lib.Context(0)
+    try:
+        for v in g["assumptions"]:
+            k, n = v["k"], v["n"]
+            d = bytes.fromhex(v["data_hex"])
+            parity, B, pad = ctx.encode(k, n, d)
+            assert (B, pad) == (v["B"], v["padlen"]), v["name"]
+            assert [p.hex() for p in parity] == v.get("parity_hex", []), v["name"]
+            padded = d + bytes(pad)
+            shares = [padded[i * B:(i + 1) * B] for i in range(k)] + list(parity)
+            order = v["decode"].get("given_order", v["decode"].get("survivors"))
+            out = ctx.decode(k, n, [shares[i] for i in order], order, B, pad)
+            assert hashlib.sha256(out).hexdigest() == v["decode"]["data_sha256"], v["name"]
+    finally:
+        ctx.close()
+
+
 def test_synthetic_challenge_sizes_match_oracle():
     """validator.rs:134-139: random sizes in [512 KiB, 8 MiB] through
     encode_chunk(&synthetic, 0): k varies (non powers of two) and padlen
