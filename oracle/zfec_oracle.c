@@ -25,11 +25,7 @@
 static uint8_t g_exp[510];
 static int g_log[256];
 static uint8_t g_inv[256];
-/* Page-aligned: with the table wherever the linker left it in .bss, the
- * byte addmul loop ran 18x slower on some GPU-box hosts (EPYC 9575F; 110 vs
- * 1990 MiB/s for the same code, layout-dependent -- tools/addmul_probe*.c,
- * DESIGN.md §5); aligned it measured fast. Layout only, same algorithm. */
-static uint8_t g_mul[256][256] __attribute__((aligned(4096)));
+static uint8_t g_mul[256][256];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 
 static void build_tables(void) {
