@@ -66,7 +66,7 @@ size_t max_kernels() {
 
 struct Entry {
   enum State { Pending, Ready, Failed };
-  State state = Pending;
+  std::atomic<State> state{Pending};  // read by launching threads without the lock
   std::string src;
   std::vector<char> code;
   std::string log;
@@ -86,8 +86,10 @@ class Jit {
   }
 
   // The entry for key, created and queued for compilation if new (nullptr
-  // when the kernel budget is spent). In Sync mode waits for the compile.
-  std::shared_ptr<Entry> get(const std::string &key, const std::string &src) {
+  // when the kernel budget is spent); src() writes the kernel source, only
+  // for a new entry. In Sync mode waits for the compile.
+  template <typename Src>
+  std::shared_ptr<Entry> get(const std::string &key, Src &&src) {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = entries_.find(key);
     std::shared_ptr<Entry> e;
@@ -96,7 +98,7 @@ class Jit {
     } else {
       if (entries_.size() >= max_kernels()) return nullptr;
       e = std::make_shared<Entry>();
-      e->src = src;
+      e->src = src();
       entries_.emplace(key, e);
       queue_.push_back(e);
       pending_++;
@@ -304,7 +306,7 @@ static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *c
   std::memcpy(&key[0], hdr, sizeof(hdr));
   std::memcpy(&key[24], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
-  auto e = J.get(key, source(k, r, coef, copy_mask, group, lds));
+  auto e = J.get(key, [&] { return source(k, r, coef, copy_mask, group, lds); });
   if (e && wait) J.wait_for(*e);
   return e;
 }
