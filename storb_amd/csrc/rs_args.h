@@ -57,11 +57,14 @@ namespace bs {
 constexpr int kBsThreads = 256;
 constexpr unsigned kBsColsPerTile = 512;
 
-// Shares per load group: whole k in flight where the registers allow it
-// (R x 8 accumulators + 2 x G x 8 loaded dwords + 30 table entries).
+// Shares per load group (R x 8 accumulators + 2 x G x 8 loaded dwords + 30
+// table entries must fit): at k = 16 with up to 8 rows, 8 shares per group
+// (196 VGPRs) streams 2 % faster than 4 (141 VGPRs) -- both run 2 waves per
+// SIMD (tools/bstune.hip, profiles/r2_bstune.txt); 16 rows leave room for 2.
 constexpr int bs_group(int K, int R) {
   return K <= 8 ? K
-                : (R >= 12 ? (K % 2 == 0 ? 2 : 1) : (K % 4 == 0 ? 4 : (K % 2 == 0 ? 2 : 1)));
+                : (R >= 12 ? (K % 2 == 0 ? 2 : 1)
+                           : (R <= 8 && K % 8 == 0 ? 8 : (K % 4 == 0 ? 4 : (K % 2 == 0 ? 2 : 1))));
 }
 }  // namespace bs
 

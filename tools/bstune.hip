@@ -1,0 +1,149 @@
+// bstune.hip -- launch-shape sweep of the bit-sliced core (rs_bitslice_core.h)
+// that both the ahead-of-time encoders and the run-time-compiled decode
+// kernels use: load-group size G (shares in flight per double-buffer half)
+// x resident-workgroup cap (LDS reservation, rs_kernels.hpp cap_lds), on the
+// wide geometries RS(16,8) (8 MiB chunks) and RS(32,16) (32 MiB chunks).
+// Every variant's output is compared bit-exactly with the product kernel's;
+// timings are interleaved rounds in one process (median of rounds).
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../storb_amd/csrc \
+//        bstune.hip -o _build/bstune
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "rs_bitslice.hpp"
+
+using namespace storb_rs;
+
+int storb_rs::wg_cap_override() { return -1; }
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,          \
+                   hipGetErrorString(e));                                      \
+      std::exit(1);                                                            \
+    }                                                                          \
+  } while (0)
+
+__global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = z ^ (z >> 31);
+  }
+}
+
+template <int K, int N, int G>
+__global__ __launch_bounds__(bs::kBsThreads) void k_bs(const ApplyArgs a) {
+  bs::bs_kernel_body<bs::EncMat<K, N>, G>(a);
+}
+
+using Fn = std::function<hipError_t(const ApplyArgs &, hipStream_t)>;
+struct V {
+  std::string name;
+  Fn fn;
+  std::vector<float> us;
+};
+
+template <int K, int N, int G>
+void add(std::vector<V> &vs) {
+  for (int cap : {0, 2, 3, 4, 6})
+    vs.push_back({"G=" + std::to_string(G) + " cap=" + std::to_string(cap),
+                  [cap](const ApplyArgs &a, hipStream_t s) {
+                    const uint64_t blocks = ((a.block / 16 + 511) / 512) * a.nstripes;
+                    return launch_lds<k_bs<K, N, G>>(blocks, 256, cap_lds(cap, 0), s, a);
+                  }, {}});
+}
+
+template <int K, int N>
+void run(const char *name, uint32_t nstripes, uint64_t B, int rounds) {
+  constexpr int R = N - K;
+  std::vector<V> vs;
+  vs.push_back({"product", [](const ApplyArgs &a, hipStream_t s) {
+                  return bs::launch_bitslice<K, N>(a, s);
+                }, {}});
+  if constexpr (K == 16) {
+    add<K, N, 2>(vs);
+    add<K, N, 4>(vs);
+    add<K, N, 8>(vs);
+  } else {
+    add<K, N, 1>(vs);
+    add<K, N, 2>(vs);
+    add<K, N, 4>(vs);
+  }
+  const uint64_t in_bytes = (uint64_t)nstripes * K * B, out_bytes = (uint64_t)nstripes * R * B;
+  uint8_t *in, *out;
+  CK(hipMalloc(&in, in_bytes));
+  CK(hipMalloc(&out, out_bytes));
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, in_bytes / 8, K);
+  ApplyArgs a{};
+  a.k = K;
+  a.r = R;
+  for (int j = 0; j < K; j++) {
+    a.in[j] = in + j * B;
+    a.in_stride[j] = K * B;
+  }
+  for (int i = 0; i < R; i++) {
+    a.out[i] = out + i * B;
+    a.out_stride[i] = R * B;
+  }
+  a.block = B;
+  a.nstripes = nstripes;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  std::vector<uint8_t> ref(out_bytes), got(out_bytes);
+  for (size_t vi = 0; vi < vs.size(); vi++) {
+    CK(hipMemset(out, 0xA5, out_bytes));
+    CK(vs[vi].fn(a, s));
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(vi ? got.data() : ref.data(), out, out_bytes, hipMemcpyDeviceToHost));
+    if (vi && std::memcmp(got.data(), ref.data(), out_bytes)) {
+      std::printf("MISMATCH %s %s\n", name, vs[vi].name.c_str());
+      std::exit(2);
+    }
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 8;
+  for (int rd = 0; rd < rounds; rd++)
+    for (auto &v : vs) {
+      CK(v.fn(a, s));
+      CK(hipEventRecord(e0, s));
+      for (int i = 0; i < reps; i++) CK(v.fn(a, s));
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1000.f / reps);
+    }
+  const double bytes = (double)in_bytes + out_bytes;
+  std::printf("%s: %.3f GB algorithmic per launch, every variant bit-exact\n", name, bytes / 1e9);
+  for (auto &v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    const float med = v.us[v.us.size() / 2];
+    std::printf("  %-14s median %8.1f us  %7.1f GB/s  %.1f%% of 8 TB/s\n", v.name.c_str(), med,
+                bytes / med / 1e3, bytes / med / 1e3 / 80.0);
+  }
+  CK(hipFree(in));
+  CK(hipFree(out));
+  CK(hipStreamDestroy(s));
+}
+
+int main(int argc, char **argv) {
+  const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
+  run<16, 24>("RS(16,8) encode 128 x 8 MiB", 128, 512 << 10, rounds);
+  run<32, 48>("RS(32,16) encode 32 x 32 MiB", 32, 1 << 20, rounds);
+  return 0;
+}
