@@ -46,14 +46,24 @@ namespace {
 
 enum class Mode { Off, Async, Sync };
 
+// STORB_RS_JIT: unset / 1 = async, sync, 0 = off; "always" (measurements
+// only) = sync and every k >= 8 matrix, VALU-bound on the table kernel or not.
 Mode mode() {
   static const Mode m = [] {
     const char *e = std::getenv("STORB_RS_JIT");
     if (!e || !*e) return Mode::Async;
-    if (std::strcmp(e, "sync") == 0) return Mode::Sync;
+    if (std::strcmp(e, "sync") == 0 || std::strcmp(e, "always") == 0) return Mode::Sync;
     return std::atoi(e) ? Mode::Async : Mode::Off;
   }();
   return m;
+}
+
+bool always() {
+  static const bool a = [] {
+    const char *e = std::getenv("STORB_RS_JIT");
+    return e && std::strcmp(e, "always") == 0;
+  }();
+  return a;
 }
 
 size_t max_kernels() {
@@ -287,7 +297,7 @@ static bool valu_bound(uint32_t k, uint32_t rows) {
       rows > static_cast<uint32_t>(kSlotR))
     return false;
   const double ops = 5.6 * k * rows + 5.0 * k;
-  return ops / (4.0 * (k + rows)) > 4.2;
+  return always() || ops / (4.0 * (k + rows)) > 4.2;
 }
 
 bool wanted(uint32_t k, uint32_t rows, uint64_t bytes) {
