@@ -286,18 +286,21 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
 
 bool enabled() { return mode() != Mode::Off; }
 
-// Worth a compiled kernel when the table kernel would be VALU-bound: its
-// ~5.6 VALU per (input, output, dword) plus ~5 selector ops per input
-// dword, over 4(k + r) bytes moved per dword column, above ~4.2 ops per
-// byte (the HBM-rate VALU budget measured in profiles/r1_valu_rate.txt is
-// ~5.2). RS(16, r >= 3), RS(32, r >= 3), RS(8, r >= 4); only for batches
-// large enough to matter.
+// Worth a compiled kernel where it beats the table kernel -- measured A/B on
+// the GPU (tools/compare_jit.sh, profiles/r2_jit_policy_ab.jsonl; decode ms,
+// table / compiled): k = 32: r = 1 0.193 / 0.191, r = 2 0.224 / 0.198,
+// r = 4 0.285 / 0.208; k = 16: r = 2 0.195 / 0.207, r = 3 0.224 / 0.225,
+// r = 4 0.227 / 0.234, r = 5 0.254 / 0.243, r = 7 0.333 / 0.260; k = 8
+// (config 3, r = 3) 0.235 / 0.254. The table kernel stays HBM-bound longer
+// at k = 16 (its tables staged in LDS) than its VALU count suggests. k = 8..11
+// with r >= 6 is the VALU model's guess (~5.5 ops per HBM byte), not
+// measured. Only for batches large enough to matter (>= 4 MiB).
 static bool valu_bound(uint32_t k, uint32_t rows) {
   if (k < 8 || k > static_cast<uint32_t>(kSlotK) || rows == 0 ||
       rows > static_cast<uint32_t>(kSlotR))
     return false;
-  const double ops = 5.6 * k * rows + 5.0 * k;
-  return always() || ops / (4.0 * (k + rows)) > 4.2;
+  const uint32_t min_rows = k >= 24 ? 2 : (k >= 12 ? 5 : 6);
+  return always() || rows >= min_rows;
 }
 
 bool wanted(uint32_t k, uint32_t rows, uint64_t bytes) {

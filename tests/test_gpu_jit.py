@@ -38,13 +38,15 @@ def launches():
 
 
 CASES = [
-    # k, n, B, stripes, erased data shares (+ parity not offered)
+    # k, n, B, stripes, erased data shares (+ parity not offered); the policy
+    # compiles k >= 24 from 2 lost rows, k = 12..23 from 5, k = 8..11 from 6
     (16, 24, 64 << 10, 4, list(range(8)), []),            # RS(16,8), every parity used
     (16, 24, 64 << 10, 4, [0, 3, 5, 9, 15], [17]),       # mixed, parity 17 missing
-    (16, 24, 3 * 8192 + 48, 40, [1, 2, 3], []),          # ragged tiles (clamped lanes)
+    (16, 24, 3 * 8192 + 48, 40, [1, 2, 3, 4, 5, 6], []),  # ragged tiles (clamped lanes)
     (32, 48, 32 << 10, 4, list(range(16)), []),           # RS(32,16), 16 lost
     (32, 48, 32 << 10, 4, [2, 7, 11, 30], [32, 33]),      # 4 lost, 2 parity also gone
-    (8, 12, 256 << 10, 4, [0, 3, 5, 6], []),              # RS(8,4) with 4 lost
+    (32, 48, 32 << 10, 4, [5, 6], []),                    # RS(32,16) with 2 lost
+    (8, 16, 256 << 10, 4, [0, 2, 3, 5, 6, 7], []),        # RS(8,8) with 6 lost
 ]
 
 
@@ -99,7 +101,7 @@ def test_jit_repair_async(ctx):
     after storb_rs_jit_wait runs the compiled one; both oracle-exact."""
     k, n, B, ns = 16, 24, 64 << 10, 6
     data_h, par_h = oracle_batch(k, n, B, ns, 21)
-    targets = [1, 6, 17, 22]
+    targets = [1, 6, 9, 17, 22]
     surv = [i for i in range(n) if i not in targets]
     for attempt in range(2):
         data = torch.from_numpy(data_h).to(DEV)
@@ -121,8 +123,9 @@ def test_jit_repair_async(ctx):
 
 
 def test_jit_not_used_where_table_kernel_is_hbm_bound(ctx):
-    """Config 3's RS(8,4) decode with 3 lost (HBM-bound on the table kernel)
-    and small batches stay on the table kernel: no compile is queued."""
+    """Config 3's RS(8,4) decode with 3 lost, RS(16,8) with 4 lost (the table
+    kernel measured faster there) and small batches stay on the table kernel:
+    no compile is queued."""
     k, n, B, ns = 8, 12, 256 << 10, 8
     data_h, par_h = oracle_batch(k, n, B, ns, 3)
     data = torch.from_numpy(data_h).to(DEV)
@@ -130,6 +133,10 @@ def test_jit_not_used_where_table_kernel_is_hbm_bound(ctx):
     st = _lib.jit_stats()
     for surv in ([1, 2, 4, 6, 7, 8, 9, 10], list(range(3, 12))):
         ctx.decode_batch_dev(k, n, B, ns, surv, data.data_ptr(), par.data_ptr(), data.data_ptr())
+    d16, p16 = oracle_batch(16, 24, 64 << 10, 4, 4)
+    d16g, p16g = torch.from_numpy(d16).to(DEV), torch.from_numpy(p16).to(DEV)
+    ctx.decode_batch_dev(16, 24, 64 << 10, 4, list(range(4, 24)), d16g.data_ptr(),
+                         p16g.data_ptr(), d16g.data_ptr())
     small = torch.from_numpy(data_h[:16 * 4096]).to(DEV)
     ctx.decode_batch_dev(16, 24, 4096, 1, list(range(8, 24)), small.data_ptr(), par.data_ptr(),
                          torch.empty_like(small).data_ptr())
@@ -138,3 +145,4 @@ def test_jit_not_used_where_table_kernel_is_hbm_bound(ctx):
     assert after["compiled"] + after["pending"] + after["failed"] == \
         st["compiled"] + st["pending"] + st["failed"]
     assert np.array_equal(data.cpu().numpy(), data_h)
+    assert np.array_equal(d16g.cpu().numpy(), d16)
