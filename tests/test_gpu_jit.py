@@ -47,6 +47,9 @@ CASES = [
     (32, 48, 32 << 10, 4, [2, 7, 11, 30], [32, 33]),      # 4 lost, 2 parity also gone
     (32, 48, 32 << 10, 4, [5, 6], []),                    # RS(32,16) with 2 lost
     (8, 16, 256 << 10, 4, [0, 2, 3, 5, 6, 7], []),        # RS(8,8) with 6 lost
+    (17, 26, 64 << 10, 4, [0, 1, 2, 3, 4, 5], []),        # odd k (last-chunk sizing), G = 1
+    (24, 36, 32 << 10, 8, [3, 20], []),                   # k = 24, G = 8
+    (20, 30, 64 << 10, 4, [1, 4, 9, 16, 19], [21]),       # k = 20, G = 4
 ]
 
 
@@ -120,6 +123,27 @@ def test_jit_repair_async(ctx):
         else:
             assert after["launches"] == st["launches"] + 1
     assert _lib.jit_stats()["failed"] == 0
+
+
+@pytest.mark.parametrize("k,n", [(24, 36), (17, 26)])
+def test_jit_encode_of_other_wide_geometries(ctx, k, n):
+    """Encodes without an ahead-of-time bit-sliced encoder (Storb sizes a short
+    last chunk to any k, piece.rs:307-317) take a compiled kernel for their
+    generator rows once it is built; before that the table kernel. Both
+    oracle-exact."""
+    B, ns = 64 << 10, 4
+    data_h, par_h = oracle_batch(k, n, B, ns, 7 * k)
+    data = torch.from_numpy(data_h).to(DEV)
+    for attempt in range(2):
+        par = torch.zeros(ns * (n - k) * B, dtype=torch.uint8, device=DEV)
+        before = launches()
+        ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(par.cpu().numpy(), par_h), attempt
+        if attempt == 0:
+            _lib.jit_wait()
+        else:
+            assert launches() == before + 1
 
 
 def test_jit_not_used_where_table_kernel_is_hbm_bound(ctx):
