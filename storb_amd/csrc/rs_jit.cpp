@@ -5,7 +5,8 @@
 // v_perm table kernel takes any matrix but spends ~5.6 VALU ops per
 // (input, output, dword); from ~3 missing rows at k = 16 (the loss of 3+
 // miners per chunk for objects of 1 GiB and up) it is VALU-bound at 27-50 %
-// of HBM peak (profiles/r1_bsbench.txt). The bit-sliced method needs the
+// of HBM peak (profiles/r1_bsbench.txt); at k = 32 the table kernel loses
+// from 2 missing rows on. The bit-sliced method needs the
 // matrix as compile-time constants (rs_bitslice_core.h), so here the host
 // writes the matrix out as a constexpr table and compiles the same core
 // header with hipRTC, once per (matrix, copy mask), on a background thread.

@@ -14,7 +14,7 @@ namespace jit {
 // STORB_RS_JIT != 0 (default on; "sync" compiles before the first launch).
 bool enabled();
 // Whether a (rows x k) matrix moving `bytes` per call is worth a compiled
-// kernel (the table kernel would be VALU-bound).
+// kernel (the table kernel measured slower on it, rs_jit.cpp).
 bool wanted(uint32_t k, uint32_t rows, uint64_t bytes);
 // Launch the compiled kernel of matrix `coef` (a.r x a.k, row-major) with
 // a's slots (a.copy[j] != null with a.ncopy: fused assembly) on stream s if

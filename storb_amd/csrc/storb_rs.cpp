@@ -219,7 +219,7 @@ static int copy_first(storb_rs_ctx *ctx, uint32_t k, const uint8_t *const *d_in,
 // into a separate chunk buffer): copy[j] != null receives input j as well;
 // rows may then be 0 (pure assembly).
 //
-// Kernel choice: under AUTO a matrix the table kernel would be VALU-bound on
+// Kernel choice: under AUTO a matrix the table kernel is measured slower on
 // runs its own compiled bit-sliced kernel once that is built (rs_jit.cpp;
 // assembly fused for any k <= 32); otherwise the table kernel, tiled into
 // kSlotR x kSlotK blocks, with the assembly fused for k <= kCopyMaxK and
