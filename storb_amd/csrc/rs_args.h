@@ -49,13 +49,35 @@ struct ApplyArgs {
 };
 
 // Launch shape of the bit-sliced kernels (rs_bitslice_core.h), shared by
-// the host launchers and the kernels. Grid: nstripes x tiles; a tile = 256
-// lanes x 32 B = 8 KiB of every share. Wave w of the tile covers 2 KiB: lane
-// l holds the 16-B columns (w*128 + l) and (w*128 + 64 + l) of the tile, so
-// each load and store instruction moves one contiguous 1 KiB per wave.
+// the host launchers and the kernels. Grid: nstripes x tiles; a tile = T
+// lanes x 32 B of every share. Wave w of the tile covers 2 KiB: lane l holds
+// the 16-B columns (w*128 + l) and (w*128 + 64 + l) of the tile, so each
+// load and store instruction moves one contiguous 1 KiB per wave.
 namespace bs {
 constexpr int kBsThreads = 256;
-constexpr unsigned kBsColsPerTile = 512;
+constexpr unsigned bs_cols_per_tile(int threads) { return 2u * static_cast<unsigned>(threads); }
+constexpr unsigned kBsColsPerTile = bs_cols_per_tile(kBsThreads);
+
+// Launch shape per (k, rows), from the sweep of workgroup size x tile
+// rotation x resident-workgroup cap: over the kernels alone
+// (tools/bstune.hip, profiles/r2_bstune_shape*.txt; tools/wide_probe.hip for
+// the access shape with no GF work) and on the product's own decode path
+// (tools/shape_ab.sh, profiles/r2_shape_ab/: bench --config 5/6 --erase E).
+// The wide shapes stream best with few bytes in flight per CU and no
+// workgroup waiting long on its slowest wave: one-wave workgroups, 6 per CU,
+// for 6+ rows at k <= 16 (RS(16,8) encode 0.267 -> 0.257 ms, 8-lost decode
+// 0.272 -> 0.257); two-wave workgroups, 3 per CU, for fewer rows (16 in + 2
+// out 0.218 -> 0.193 ms, + 4 out 0.243 -> 0.217); 4 per CU for 8+ rows at
+// k > 16 (48 streams: RS(32,16) 16-lost decode 0.282 -> 0.276 ms). swz:
+// tile rotation per stripe (bs_kernel_body); threads <= 128 with
+// amdgpu_waves_per_eu(2) keeps 2 waves per SIMD.
+struct BsShape {
+  int threads, swz, cap;
+};
+constexpr BsShape bs_shape(int K, int R) {
+  return K <= 16 ? (R >= 6 ? BsShape{64, 1, 6} : BsShape{128, 0, 3})
+                 : (R >= 8 ? BsShape{128, 0, 4} : BsShape{128, 0, 3});
+}
 
 // Shares per load group (R x 8 accumulators + 2 x G x 8 loaded dwords + 30
 // table entries must fit): at k = 16 with up to 8 rows, 8 shares per group

@@ -97,28 +97,30 @@ struct EncMat {
   static constexpr Bits<K_, N_> net = make_bits<K_, N_>();
 };
 
-// Launch shape per geometry.
+// Launch shape per geometry (rs_args.h bs_shape).
 template <int K, int N>
 struct BsTune {
-  // resident workgroups per CU (rs_kernels.hpp wg_cap): RS(16,8) 0.281 ->
-  // 0.275 ms at 2 (= 3; tools/occ_sweep.py, profiles/r1_occupancy.txt)
-  static constexpr int OCC = K == 16 ? 2 : 0;
+  static constexpr BsShape S = bs_shape(K, N - K);
+  static constexpr int T = S.threads, SWZ = S.swz, OCC = S.cap;
   static constexpr int G = bs_group(K, N - K);
 };
 
 template <int K, int N>
-__global__ __launch_bounds__(kBsThreads) void rs_encode_bitslice(const ApplyArgs a) {
-  bs_kernel_body<EncMat<K, N>, BsTune<K, N>::G>(a);
+__global__ __launch_bounds__((BsTune<K, N>::T)) __attribute__((amdgpu_waves_per_eu(2))) void
+rs_encode_bitslice(const ApplyArgs a) {
+  using C = BsTune<K, N>;
+  bs_kernel_body<EncMat<K, N>, C::G, C::T, C::SWZ>(a);
 }
 
 template <int K, int N>
 hipError_t launch_bitslice(const ApplyArgs &a, hipStream_t s) {
+  using C = BsTune<K, N>;
+  constexpr uint64_t cpt = bs_cols_per_tile(C::T);
   const uint64_t cols = a.block >> 4;
-  const uint64_t blocks = ((cols + 511) / 512) * a.nstripes;
+  const uint64_t blocks = ((cols + cpt - 1) / cpt) * a.nstripes;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  return launch_lds<rs_encode_bitslice<K, N>>(blocks, 256,
-                                               cap_lds(wg_cap(BsTune<K, N>::OCC), 0), s, a);
+  return launch_lds<rs_encode_bitslice<K, N>>(blocks, C::T, cap_lds(wg_cap(C::OCC), 0), s, a);
 }
 
 }  // namespace bs

@@ -216,14 +216,20 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
   }
 }
 
-// Grid: nstripes x tiles of kBsColsPerTile 16-B columns (rs_args.h).
-template <class M, int G>
+// Grid: nstripes x tiles of bs_cols_per_tile(T) 16-B columns (rs_args.h);
+// T lanes per workgroup, each wave covering 2 KiB of every share. SWZ = 1
+// rotates the tile order of stripe s by s * (tiles / 8 + 1), so the
+// workgroups of neighbouring stripes that run at the same moment stream
+// from different offsets of their shares (tools/wide_probe.hip).
+template <class M, int G, int T = kBsThreads, int SWZ = 0>
 __device__ __forceinline__ void bs_kernel_body(const ApplyArgs &a) {
+  constexpr uint32_t CPT = bs_cols_per_tile(T);
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
-  const uint32_t tps = (cols + kBsColsPerTile - 1) / kBsColsPerTile;
+  const uint32_t tps = (cols + CPT - 1) / CPT;
   const uint32_t stripe = blockIdx.x / tps;
-  const uint32_t tile = blockIdx.x - stripe * tps;
-  const uint32_t v0 = tile * kBsColsPerTile + (threadIdx.x >> 6) * 128 + (threadIdx.x & 63);
+  uint32_t tile = blockIdx.x - stripe * tps;
+  if constexpr (SWZ == 1) tile = (tile + stripe * (tps / 8 + 1)) % tps;
+  const uint32_t v0 = tile * CPT + (threadIdx.x >> 6) * 128 + (threadIdx.x & 63);
   bs_tile<M, G>(a, stripe, v0, cols);
 }
 

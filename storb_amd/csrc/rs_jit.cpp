@@ -196,6 +196,12 @@ class Jit {
           std::fputs(e->src.c_str(), f);
           std::fclose(f);
         }
+        // the code object too (llvm-readelf --notes: .vgpr_count, .sgpr_count)
+        if (ok)
+          if (FILE *f = std::fopen((path + ".co").c_str(), "wb")) {
+            std::fwrite(e->code.data(), 1, e->code.size(), f);
+            std::fclose(f);
+          }
       }
       cv_.notify_all();
     }
@@ -239,15 +245,27 @@ Jit &jit() {
   return j;
 }
 
-// Resident workgroups per CU (the LDS reservation of rs_kernels.hpp cap_lds,
-// baked into the kernel as static LDS): the bit-sliced encoder's tuning,
-// 2 at k = 16, uncapped at k = 32 (profiles/r1_occupancy.txt).
-int occ_cap(uint32_t k) { return wg_cap(k == 16 ? 2 : 0); }
+// Launch shape (rs_args.h bs_shape, shared with the ahead-of-time
+// encoders); the resident-workgroup cap is baked into the kernel as static
+// LDS (rs_kernels.hpp cap_lds).
+// STORB_RS_JIT_SHAPE="threads,swz,cap" overrides it for every compiled
+// kernel (launch-shape A/B on the real decode path without a rebuild).
+bs::BsShape shape(uint32_t k, uint32_t r) {
+  bs::BsShape s = bs::bs_shape(static_cast<int>(k), static_cast<int>(r));
+  if (const char *e = std::getenv("STORB_RS_JIT_SHAPE")) {
+    int t = 0, w = 0, c = 0;
+    if (std::sscanf(e, "%d,%d,%d", &t, &w, &c) == 3 && (t == 64 || t == 128 || t == 256) &&
+        (w == 0 || w == 1) && c >= 0 && c <= 32)
+      s = bs::BsShape{t, w, c};
+  }
+  s.cap = wg_cap(s.cap);
+  return s;
+}
 
 // The kernel source for a (rows x k) matrix: bit b' of row[p][j][b] is bit b
 // of coef[p][j] * 2^b' (the GF(2) matrix of multiplication by coef[p][j]).
 std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask,
-                   int group, size_t lds) {
+                   int group, const bs::BsShape &sh, size_t lds) {
   const GF256 &g = gf();
   std::string s;
   s.reserve(64 + static_cast<size_t>(rows) * k * 40);
@@ -272,14 +290,18 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
     s += '}';
   }
   s += "}};\n};\n}  // namespace\n";
-  s += "extern \"C\" __global__ __launch_bounds__(256) void storb_bs_jit(const "
-       "storb_rs::ApplyArgs a) {\n";
+  // 2 waves per SIMD (<= 256 registers): without the hint, 64- and 128-lane
+  // workgroups let the allocator take 257 at k = 32 (1 wave per SIMD)
+  s += "extern \"C\" __global__ __launch_bounds__(" + std::to_string(sh.threads) +
+       ") __attribute__((amdgpu_waves_per_eu(2))) void storb_bs_jit(const storb_rs::ApplyArgs "
+       "a) {\n";
   if (lds >= 4) {
     // Static LDS reserving 160 KiB / cap per workgroup (occupancy cap).
     s += "  __shared__ unsigned occ_pad[" + std::to_string(lds / 4) + "];\n";
     s += "  asm volatile(\"\" :: \"s\"(occ_pad));  // keeps the unused array allocated\n";
   }
-  s += "  storb_rs::bs::bs_kernel_body<JitMat, " + std::to_string(group) + ">(a);\n}\n";
+  s += "  storb_rs::bs::bs_kernel_body<JitMat, " + std::to_string(group) + ", " +
+       std::to_string(sh.threads) + ", " + std::to_string(sh.swz) + ">(a);\n}\n";
   return s;
 }
 
@@ -288,19 +310,22 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
 bool enabled() { return mode() != Mode::Off; }
 
 // Worth a compiled kernel where it beats the table kernel -- measured A/B on
-// the GPU (tools/compare_jit.sh, profiles/r2_jit_policy_ab.jsonl; decode ms,
-// table / compiled): k = 32: r = 1 0.193 / 0.191, r = 2 0.224 / 0.198,
-// r = 4 0.285 / 0.208; k = 16: r = 2 0.195 / 0.207, r = 3 0.224 / 0.225,
-// r = 4 0.227 / 0.234, r = 5 0.254 / 0.243, r = 7 0.333 / 0.260; k = 8
-// (config 3, r = 3) 0.235 / 0.254. The table kernel stays HBM-bound longer
-// at k = 16 (its tables staged in LDS) than its VALU count suggests. k = 8..11
+// the GPU with the launch shapes of rs_args.h bs_shape (tools/compare_jit.sh,
+// STORB_RS_JIT=0 vs =always, profiles/r2_jit_policy_ab2/; bench decode leg
+// ms, table / compiled): k = 16: r = 2 0.195 / 0.189, r = 3 0.219 / 0.204,
+// r = 4 0.235 / 0.218, r = 8 0.397 / 0.256; k = 32: r = 2 0.230 / 0.187,
+// r = 4 0.295 / 0.202, r = 16 0.732 / 0.269; k = 8 (config 3, r = 3) 0.236 /
+// 0.235-0.246 over six launch shapes (profiles/r2_shape_ab/), so the table
+// kernel keeps it. Before the launch-shape sweep the table kernel won at k =
+// 16 up to 4 rows (profiles/r2_jit_policy_ab.jsonl). One row (repair of a
+// single share): 0.193 / 0.191 at k = 32, left to the table kernel. k = 8..11
 // with r >= 6 is the VALU model's guess (~5.5 ops per HBM byte), not
 // measured. Only for batches large enough to matter (>= 4 MiB).
 static bool valu_bound(uint32_t k, uint32_t rows) {
   if (k < 8 || k > static_cast<uint32_t>(kSlotK) || rows == 0 ||
       rows > static_cast<uint32_t>(kSlotR))
     return false;
-  const uint32_t min_rows = k >= 24 ? 2 : (k >= 12 ? 5 : 6);
+  const uint32_t min_rows = k >= 12 ? 2 : 6;
   return always() || rows >= min_rows;
 }
 
@@ -313,14 +338,16 @@ bool wanted(uint32_t k, uint32_t rows, uint64_t bytes) {
 static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *coef,
                                         uint64_t copy_mask, bool wait) {
   const int group = bs::bs_group(static_cast<int>(k), static_cast<int>(r));
-  const size_t lds = cap_lds(occ_cap(k), 0);
-  std::string key(24 + static_cast<size_t>(r) * k, '\0');
-  const uint64_t hdr[3] = {(static_cast<uint64_t>(k) << 32) | r, copy_mask,
-                           (static_cast<uint64_t>(group) << 32) | lds};
+  const bs::BsShape sh = shape(k, r);
+  const size_t lds = cap_lds(sh.cap, 0);
+  std::string key(32 + static_cast<size_t>(r) * k, '\0');
+  const uint64_t hdr[4] = {(static_cast<uint64_t>(k) << 32) | r, copy_mask,
+                           (static_cast<uint64_t>(group) << 32) | lds,
+                           (static_cast<uint64_t>(sh.threads) << 32) | static_cast<uint32_t>(sh.swz)};
   std::memcpy(&key[0], hdr, sizeof(hdr));
-  std::memcpy(&key[24], coef, static_cast<size_t>(r) * k);
+  std::memcpy(&key[32], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
-  auto e = J.get(key, [&] { return source(k, r, coef, copy_mask, group, lds); });
+  auto e = J.get(key, [&] { return source(k, r, coef, copy_mask, group, sh, lds); });
   if (e && wait) J.wait_for(*e);
   return e;
 }
@@ -332,7 +359,9 @@ hipError_t try_launch(int device, const ApplyArgs &a, const uint8_t *coef, hipSt
       a.r > static_cast<uint32_t>(kSlotR) || a.accumulate || !vector_ok(a))
     return hipSuccess;
   const uint64_t cols = a.block >> 4;
-  const uint64_t blocks = ((cols + bs::kBsColsPerTile - 1) / bs::kBsColsPerTile) * a.nstripes;
+  const bs::BsShape sh = shape(a.k, a.r);
+  const uint64_t cpt = bs::bs_cols_per_tile(sh.threads);
+  const uint64_t blocks = ((cols + cpt - 1) / cpt) * a.nstripes;
   if (blocks == 0 || blocks > 0x7FFFFFFFull) return hipSuccess;  // table kernel handles it
   uint64_t copy_mask = 0;
   for (uint32_t j = 0; a.ncopy && j < a.k; j++)
@@ -348,7 +377,8 @@ hipError_t try_launch(int device, const ApplyArgs &a, const uint8_t *coef, hipSt
   if (r != hipSuccess) return r;
   ApplyArgs arg = a;
   void *params[] = {&arg};
-  r = hipModuleLaunchKernel(f, static_cast<unsigned>(blocks), 1, 1, bs::kBsThreads, 1, 1, 0, s,
+  r = hipModuleLaunchKernel(f, static_cast<unsigned>(blocks), 1, 1,
+                            static_cast<unsigned>(sh.threads), 1, 1, 0, s,
                             params, nullptr);
   if (r != hipSuccess) return r;
   J.launches++;

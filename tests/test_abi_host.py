@@ -107,12 +107,12 @@ def test_jit_compiles_decode_kernels_without_gpu():
     """The run-time-compiled decode kernels build with hipRTC on the host
     (no GPU): RS(16,8) with every data share lost, in place and assembled,
     and RS(32,16) with 16 lost. Matrices the policy does not want (RS(4,2),
-    RS(8,4) with 3 lost) queue nothing."""
+    RS(8,4) with 3 lost, one lost share at k = 16) queue nothing."""
     from storb_amd import _lib
     before = _lib.jit_stats()
     _lib.jit_prepare_decode(4, 6, [2, 3, 4, 5])
     _lib.jit_prepare_decode(8, 12, [1, 2, 4, 6, 7, 8, 9, 10, 11])
-    _lib.jit_prepare_decode(16, 24, list(range(4, 24)))  # 4 lost: table kernel faster
+    _lib.jit_prepare_decode(16, 24, list(range(1, 24)))  # 1 lost: table kernel
     assert _lib.jit_stats()["compiled"] == before["compiled"]
     _lib.jit_prepare_decode(16, 24, list(range(8, 24)))
     _lib.jit_prepare_decode(16, 24, [1, 2, 3, 5, 8, 13, 16, 17, 18, 19, 20, 21, 22, 23, 4, 6],

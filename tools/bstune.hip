@@ -44,9 +44,9 @@ __global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
   }
 }
 
-template <int K, int N, int G>
-__global__ __launch_bounds__(bs::kBsThreads) void k_bs(const ApplyArgs a) {
-  bs::bs_kernel_body<bs::EncMat<K, N>, G>(a);
+template <int K, int N, int G, int T, int SWZ>
+__global__ __launch_bounds__(T) void k_bs(const ApplyArgs a) {
+  bs::bs_kernel_body<bs::EncMat<K, N>, G, T, SWZ>(a);
 }
 
 using Fn = std::function<hipError_t(const ApplyArgs &, hipStream_t)>;
@@ -56,59 +56,73 @@ struct V {
   std::vector<float> us;
 };
 
-template <int K, int N, int G>
-void add(std::vector<V> &vs) {
-  for (int cap : {0, 2, 3, 4, 6})
-    vs.push_back({"G=" + std::to_string(G) + " cap=" + std::to_string(cap),
+// Workgroup size T (lanes; each wave streams 2 KiB of every share) x
+// tile rotation per stripe (SWZ) x resident-workgroup cap, for load group G.
+template <int K, int N, int G, int T, int SWZ>
+void add(std::vector<V> &vs, std::initializer_list<int> caps) {
+  for (int cap : caps)
+    vs.push_back({"G=" + std::to_string(G) + " T=" + std::to_string(T) + " swz=" +
+                      std::to_string(SWZ) + " cap=" + std::to_string(cap),
                   [cap](const ApplyArgs &a, hipStream_t s) {
-                    const uint64_t blocks = ((a.block / 16 + 511) / 512) * a.nstripes;
-                    return launch_lds<k_bs<K, N, G>>(blocks, 256, cap_lds(cap, 0), s, a);
+                    const uint64_t cpt = bs::bs_cols_per_tile(T);
+                    const uint64_t blocks = ((a.block / 16 + cpt - 1) / cpt) * a.nstripes;
+                    return launch_lds<k_bs<K, N, G, T, SWZ>>(blocks, T, cap_lds(cap, 0), s, a);
                   }, {}});
 }
 
+// dec = false: encode layout (k data shares in, n - k parity shares out, each
+// region packed per stripe). dec = true: the in-place decode layout of
+// bench.py --erase R (data shares 0..R-1 lost, rebuilt into their slots of the
+// data region from data shares R..K-1 and parity shares 0..R-1), so reads and
+// writes share the data region as they do in the product.
 template <int K, int N>
-void run(const char *name, uint32_t nstripes, uint64_t B, int rounds) {
+void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec = false) {
   constexpr int R = N - K;
   std::vector<V> vs;
-  vs.push_back({"product", [](const ApplyArgs &a, hipStream_t s) {
-                  return bs::launch_bitslice<K, N>(a, s);
-                }, {}});
-  if constexpr (K == 16) {
-    add<K, N, 2>(vs);
-    add<K, N, 4>(vs);
-    add<K, N, 8>(vs);
-  } else {
-    add<K, N, 1>(vs);
-    add<K, N, 2>(vs);
-    add<K, N, 4>(vs);
-  }
+  if (!dec)
+    vs.push_back({"product", [](const ApplyArgs &a, hipStream_t s) {
+                    return bs::launch_bitslice<K, N>(a, s);
+                  }, {}});
+  constexpr int G = bs::bs_group(K, R);
+  add<K, N, G, 256, 0>(vs, {0, 2});
+  add<K, N, G, 128, 0>(vs, {3, 4});
+  add<K, N, G, 128, 1>(vs, {4});
+  add<K, N, G, 64, 0>(vs, {4, 5, 6, 8});
+  add<K, N, G, 64, 1>(vs, {4, 5, 6, 8});
+  // parity region: Storb's n - k = k / 2 shares per stripe in the decode layout
+  constexpr int P = K / 2;
   const uint64_t in_bytes = (uint64_t)nstripes * K * B, out_bytes = (uint64_t)nstripes * R * B;
+  const uint64_t par_bytes = dec ? (uint64_t)nstripes * P * B : out_bytes;
   uint8_t *in, *out;
   CK(hipMalloc(&in, in_bytes));
-  CK(hipMalloc(&out, out_bytes));
+  CK(hipMalloc(&out, par_bytes));
   hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, in_bytes / 8, K);
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)out, par_bytes / 8, N);
   ApplyArgs a{};
   a.k = K;
   a.r = R;
   for (int j = 0; j < K; j++) {
-    a.in[j] = in + j * B;
-    a.in_stride[j] = K * B;
+    const bool par = dec && j >= K - R;
+    a.in[j] = par ? out + (j - (K - R)) * B : in + (dec ? j + R : j) * B;
+    a.in_stride[j] = par ? P * B : K * B;
   }
   for (int i = 0; i < R; i++) {
-    a.out[i] = out + i * B;
-    a.out_stride[i] = R * B;
+    a.out[i] = dec ? in + i * B : out + i * B;
+    a.out_stride[i] = dec ? K * B : R * B;
   }
   a.block = B;
   a.nstripes = nstripes;
+  uint8_t *res = dec ? in : out;
+  const uint64_t res_bytes = dec ? in_bytes : out_bytes;
   hipStream_t s;
   CK(hipStreamCreate(&s));
-  std::vector<uint8_t> ref(out_bytes), got(out_bytes);
+  std::vector<uint8_t> ref(res_bytes), got(res_bytes);
   for (size_t vi = 0; vi < vs.size(); vi++) {
-    CK(hipMemset(out, 0xA5, out_bytes));
+    if (!dec) CK(hipMemset(out, 0xA5, out_bytes));
     CK(vs[vi].fn(a, s));
     CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(vi ? got.data() : ref.data(), out, out_bytes, hipMemcpyDeviceToHost));
-    if (vi && std::memcmp(got.data(), ref.data(), out_bytes)) {
+    CK(hipMemcpy(vi ? got.data() : ref.data(), res, res_bytes, hipMemcpyDeviceToHost));
+    if (vi && std::memcmp(got.data(), ref.data(), res_bytes)) {
       std::printf("MISMATCH %s %s\n", name, vs[vi].name.c_str());
       std::exit(2);
     }
@@ -128,12 +142,12 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       v.us.push_back(ms * 1000.f / reps);
     }
-  const double bytes = (double)in_bytes + out_bytes;
+  const double bytes = (double)in_bytes + out_bytes;  // k*B read + r*B written, either layout
   std::printf("%s: %.3f GB algorithmic per launch, every variant bit-exact\n", name, bytes / 1e9);
   for (auto &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
-    std::printf("  %-14s median %8.1f us  %7.1f GB/s  %.1f%% of 8 TB/s\n", v.name.c_str(), med,
+    std::printf("  %-26s median %8.1f us  %7.1f GB/s  %.1f%% of 8 TB/s\n", v.name.c_str(), med,
                 bytes / med / 1e3, bytes / med / 1e3 / 80.0);
   }
   CK(hipFree(in));
@@ -143,7 +157,17 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds) {
 
 int main(int argc, char **argv) {
   const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
-  run<16, 24>("RS(16,8) encode 128 x 8 MiB", 128, 512 << 10, rounds);
-  run<32, 48>("RS(32,16) encode 32 x 32 MiB", 32, 1 << 20, rounds);
+  const int which = argc > 2 ? std::atoi(argv[2]) : 0;  // 0 all, 1 encode, 2 decode
+  if (which != 2) {
+    run<16, 24>("RS(16,8) encode 128 x 8 MiB", 128, 512 << 10, rounds);
+    run<32, 48>("RS(32,16) encode 32 x 32 MiB", 32, 1 << 20, rounds);
+  }
+  if (which != 1) {
+    run<16, 18>("decode k=16, 2 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    run<16, 20>("decode k=16, 4 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    run<16, 24>("decode k=16, 8 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    run<32, 34>("decode k=32, 2 lost, 32 x 32 MiB (in place)", 32, 1 << 20, rounds, true);
+    run<32, 48>("decode k=32, 16 lost, 32 x 32 MiB (in place)", 32, 1 << 20, rounds, true);
+  }
   return 0;
 }
