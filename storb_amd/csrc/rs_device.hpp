@@ -415,9 +415,25 @@ inline uint64_t tile_blocks(const ApplyArgs &a) {
   return ((cols + TILE - 1) / TILE) * a.nstripes;
 }
 
+// Buckets the benches run that can also launch with 64- or 128-lane
+// workgroups (STORB_RS_TABLE_T, rs_kernels.hpp; the cap scaled to the same
+// waves per CU) for launch-shape A/B in the product.
+template <int KM, int RM>
+constexpr bool kAltThreads = (KM == 4 && RM <= 2) || (KM == 8 && (RM == 3 || RM == 4)) ||
+                             (KM == 2 && RM == 1) || (KM == 16 && RM <= 2);
+
 template <int KM, int RM>
 hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
   using C = Tune<KM, RM>;
+  if constexpr (kAltThreads<KM, RM>) {
+    const int t = table_threads_override();
+    if (t == 64)
+      return launch_perm<KM, RM, 64, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC * 4,
+                                                                        C::OCC_COPY * 4);
+    if (t == 128)
+      return launch_perm<KM, RM, 128, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC * 2,
+                                                                         C::OCC_COPY * 2);
+  }
   return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC, C::OCC_COPY);
 }
 

@@ -79,6 +79,15 @@ int wg_cap_override() {
   return v;
 }
 
+int table_threads_override() {
+  static const int v = [] {
+    const char *e = std::getenv("STORB_RS_TABLE_T");
+    const int t = e && *e ? std::atoi(e) : 0;
+    return (t == 64 || t == 128) ? t : 0;
+  }();
+  return v;
+}
+
 bool vector_ok(const ApplyArgs &a) {
   if (a.block % 16) return false;
   for (uint32_t j = 0; a.ncopy && j < a.k; j++)

@@ -34,6 +34,9 @@ enum class Variant { Perm = 1, Lds = 2 };
 // STORB_RS_WG_PER_CU overrides every kernel's cap (0 = uncapped).
 constexpr size_t kLdsPerCu = 160u << 10;
 int wg_cap_override();  // -1 when unset
+// STORB_RS_TABLE_T = 64 / 128: lanes per workgroup of the table kernel's
+// benchmarked buckets (rs_device.hpp go_perm), for A/B; 0 when unset.
+int table_threads_override();
 inline int wg_cap(int tuned) {
   const int o = wg_cap_override();
   return o >= 0 ? o : tuned;

@@ -22,6 +22,7 @@ trace() {  # name, bench args...
   echo "traced $name"
 }
 trace config2
+trace config5 --config 5
 trace config5_erase8 --config 5 --erase 8
 trace config6_erase16 --config 6 --erase 16
 timeout -k 10 400 python3 bench.py > "$OUT/bench_default.log" 2>&1
