@@ -85,15 +85,37 @@ struct Entry {
   std::vector<hipModule_t> modules;
 };
 
+class Jit;
+Jit &jit();
+
 class Jit {
  public:
-  ~Jit() {
+  ~Jit() { shutdown(); }
+
+  // Stop compiling: queued entries fail, the compile in flight finishes,
+  // the worker is joined. Runs at process exit from an atexit handler
+  // registered after hipRTC / comgr have built their static state (a
+  // warm-up compile before the worker starts, and again after every
+  // compile), so -- exit handlers run in reverse order of registration --
+  // before that state is torn down. Without it a compile still running at
+  // exit used comgr's destroyed state: "LLVM ERROR: Invalid size request on
+  // a scalable vector" + abort on the GPU box (tools/fuzz.py), a hang here.
+  void shutdown() {
+    std::thread w;
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
+      for (auto &e : queue_) {
+        e->state = Entry::Failed;
+        failed_++;
+        pending_--;
+      }
+      queue_.clear();
+      if (worker_.joinable() && worker_.get_id() != std::this_thread::get_id())
+        w = std::move(worker_);
     }
     cv_.notify_all();
-    if (worker_.joinable()) worker_.join();
+    if (w.joinable()) w.join();
   }
 
   // The entry for key, created and queued for compilation if new (nullptr
@@ -113,7 +135,10 @@ class Jit {
       entries_.emplace(key, e);
       queue_.push_back(e);
       pending_++;
-      if (!worker_.joinable()) worker_ = std::thread([this] { run(); });
+      if (!worker_.joinable() && !stop_) {
+        warm_up();
+        worker_ = std::thread([this] { run(); });
+      }
       cv_.notify_all();
     }
     if (mode() == Mode::Sync) cv_.wait(lk, [&] { return e->state != Entry::Pending; });
@@ -176,6 +201,7 @@ class Jit {
       std::vector<char> code;
       std::string log;
       const bool ok = compile(e->src, code, log);
+      register_exit_hook();
       const double ms =
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       {
@@ -205,6 +231,19 @@ class Jit {
       }
       cv_.notify_all();
     }
+  }
+
+  static void register_exit_hook() { std::atexit([] { jit().shutdown(); }); }
+
+  // One tiny hipRTC compile in the calling thread before the first worker
+  // starts (once per process, ~0.1-0.3 s): comgr builds its static state
+  // here, then the exit hook is registered after it.
+  void warm_up() {
+    std::vector<char> code;
+    std::string log;
+    compile("extern \"C\" __global__ void storb_jit_warm(unsigned *p) { p[threadIdx.x] = 1u; }\n",
+            code, log);
+    register_exit_hook();
   }
 
   static bool compile(const std::string &src, std::vector<char> &code, std::string &log) {

@@ -124,3 +124,26 @@ def test_jit_compiles_decode_kernels_without_gpu():
     # the same pattern again is a cache hit
     _lib.jit_prepare_decode(16, 24, list(range(8, 24)))
     assert _lib.jit_stats()["compiled"] == st["compiled"]
+
+
+def test_exit_with_jit_compiles_in_flight():
+    """A process that exits while decode kernels are still queued or compiling
+    exits cleanly: the JIT's exit hook (registered after hipRTC's own static
+    state) fails the queued entries and waits out the compile in flight.
+    Before, the compile ran on into comgr's destroyed state: an LLVM abort on
+    the GPU box (tools/fuzz.py), a hang here."""
+    import subprocess
+    import sys
+    code = (
+        "import random\n"
+        "from storb_amd import _lib\n"
+        "rng = random.Random(7)\n"
+        "for _ in range(6):\n"
+        "    lost = rng.sample(range(32), rng.randint(2, 16))\n"
+        "    _lib.jit_prepare_decode(32, 48, [x for x in range(48) if x not in lost])\n"
+        "print('queued', _lib.jit_stats()['pending'])\n")
+    env = dict(os.environ, PYTHONPATH=ROOT, AMD_COMGR_CACHE="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "queued" in r.stdout

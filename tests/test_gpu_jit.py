@@ -39,7 +39,9 @@ def launches():
 
 CASES = [
     # k, n, B, stripes, erased data shares (+ parity not offered); the policy
-    # compiles k >= 24 from 2 lost rows, k = 12..23 from 5, k = 8..11 from 6
+    # compiles k >= 12 from 2 lost rows, k = 8..11 from 6. Launch shapes
+    # (rs_args.h bs_shape): 64 lanes rotated for 6+ rows at k <= 16, 128 lanes
+    # below and at k > 16.
     (16, 24, 64 << 10, 4, list(range(8)), []),            # RS(16,8), every parity used
     (16, 24, 64 << 10, 4, [0, 3, 5, 9, 15], [17]),       # mixed, parity 17 missing
     (16, 24, 3 * 8192 + 48, 40, [1, 2, 3, 4, 5, 6], []),  # ragged tiles (clamped lanes)
@@ -50,6 +52,10 @@ CASES = [
     (17, 26, 64 << 10, 4, [0, 1, 2, 3, 4, 5], []),        # odd k (last-chunk sizing), G = 1
     (24, 36, 32 << 10, 8, [3, 20], []),                   # k = 24, G = 8
     (20, 30, 64 << 10, 4, [1, 4, 9, 16, 19], [21]),       # k = 20, G = 4
+    (16, 24, 3 * 8192 + 48, 40, [0, 1], []),              # 2 lost: 128-lane shape, ragged
+    (16, 24, 4096 + 16, 64, [4, 5, 6], []),               # last tile of one column
+    (12, 18, 64 << 10, 8, [2, 9], [13]),                  # k = 12 from 2 rows
+    (16, 24, 48 << 10, 9, list(range(6)), []),            # 6 rows: 64-lane rotated, 9 stripes
 ]
 
 
