@@ -44,6 +44,8 @@ extern "C" {
 #define STORB_RS_EDEVICE 3    /* HIP runtime failure (see storb_rs_last_error) */
 #define STORB_RS_ENOMEM 4     /* device or pinned allocation failed */
 #define STORB_RS_ENODEV 5     /* no usable gfx950 device */
+#define STORB_RS_EAGAIN 6     /* storb_rs_op_test: the op's device work is still running */
+#define STORB_RS_EBUSY 7      /* 64 unfinished async ops on the context already */
 
 #define STORB_RS_MAX_SHARES 256 /* zfec: n <= 256 */
 
@@ -225,8 +227,8 @@ int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant);
 
 /* Run-time-compiled bit-sliced kernels. Decode and repair apply rows of the
  * inverted survivor matrix, known only when the erasure pattern is. Under
- * AUTO, a matrix the table kernel is measured slower on (k >= 24 with >= 2
- * rows, k = 12..23 with >= 5, k = 8..11 with >= 6; batches >= 4 MiB)
+ * AUTO, a matrix the table kernel is measured slower on (k >= 12 with >= 2
+ * rows, k = 8..11 with >= 6; batches >= 4 MiB)
  * gets its own bit-sliced kernel, compiled with hipRTC on a background thread
  * and cached for the process; calls made while it compiles run the table
  * kernel. STORB_RS_JIT=0 disables, =sync compiles before the first launch;
@@ -250,6 +252,38 @@ int storb_rs_jit_wait(void);
  * failed. */
 int storb_rs_jit_prepare_decode(uint32_t k, uint32_t n, const uint32_t *share_idx,
                                 uint32_t nshares, int assemble, int wait);
+
+/* Asynchronous single-chunk calls. The reference calls encode_chunk /
+ * decode_chunk synchronously inside async tasks (upload.rs:418-420,
+ * download.rs:464; SURVEY 8(b) names an async variant as the next step); these
+ * let an integration await the GPU instead of blocking a worker thread.
+ * Arguments and results are those of storb_rs_encode / storb_rs_decode. The
+ * call validates, copies the input into page-locked staging of the op's own
+ * (the caller may reuse `data` / `shares` as soon as it returns), queues the
+ * kernel on a stream of the op's own and returns; block_out / padlen_out are
+ * set at once. The output buffers must stay valid until storb_rs_op_finish.
+ * notify(user), if not NULL, is called exactly once when the op's device work
+ * is done -- from a HIP runtime thread (it must only wake a waiter: no calls
+ * into this library or HIP), or before the call returns when there is no
+ * device work (k = 1, nothing missing). storb_rs_op_test polls (STORB_RS_OK
+ * when done, STORB_RS_EAGAIN while running); storb_rs_op_finish waits if
+ * needed, writes the outputs, frees the op and returns its result. Finish
+ * every op exactly once, before destroying its context. Ops of a context run
+ * concurrently (one stream and staging slot each, reused after finish); with
+ * 64 unfinished the call returns STORB_RS_EBUSY. On any error no op is
+ * returned. */
+typedef struct storb_rs_op storb_rs_op;
+typedef void (*storb_rs_notify_fn)(void *user);
+int storb_rs_encode_async(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                          size_t len, uint8_t *const *parity_out, size_t *block_out,
+                          size_t *padlen_out, storb_rs_notify_fn notify, void *user,
+                          storb_rs_op **op);
+int storb_rs_decode_async(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                          const uint8_t *const *shares, const uint32_t *share_idx,
+                          uint32_t nshares, size_t block, size_t padlen, uint8_t *out,
+                          storb_rs_notify_fn notify, void *user, storb_rs_op **op);
+int storb_rs_op_test(const storb_rs_op *op);
+int storb_rs_op_finish(storb_rs_op *op);
 
 /* Synchronise the context's own streams and the HIP null stream of its
  * device (where device calls given hip_stream = NULL run). Work the caller

@@ -54,6 +54,9 @@ class JitStats(C.Structure):
                 ("launches", C.c_uint64), ("fallbacks", C.c_uint64), ("compile_ms", C.c_double)]
 
 
+NOTIFY_FN = C.CFUNCTYPE(None, vp)  # storb_rs_notify_fn
+
+
 def _declare(L):
     L.storb_rs_version.restype = C.c_char_p
     L.storb_rs_strerror.restype = C.c_char_p
@@ -107,6 +110,14 @@ def _declare(L):
     L.storb_rs_host_register.argtypes = [vp, sz]
     L.storb_rs_host_unregister.argtypes = [vp]
     L.storb_rs_host_is_pinned.argtypes = [vp, sz]
+    L.storb_rs_encode_async.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.POINTER(vp),
+                                        C.POINTER(sz), C.POINTER(sz), NOTIFY_FN, vp,
+                                        C.POINTER(vp)]
+    L.storb_rs_decode_async.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(vp),
+                                        C.POINTER(C.c_uint32), C.c_uint32, sz, sz, vp,
+                                        NOTIFY_FN, vp, C.POINTER(vp)]
+    L.storb_rs_op_test.argtypes = [vp]
+    L.storb_rs_op_finish.argtypes = [vp]
     L.storb_rs_set_kernel.argtypes = [vp, C.c_int]
     L.storb_rs_sync.argtypes = [vp]
     L.storb_rs_jit_stats.argtypes = [C.POINTER(JitStats)]
@@ -328,6 +339,45 @@ class Context:
                                    out.ctypes.data)
         self._check(rc, "storb_rs_decode")
 
+    # ------------------------------------------------ asynchronous calls
+    def encode_async(self, k: int, n: int, data, notify=None, parity=None) -> "AsyncOp":
+        """storb_rs_encode_async: returns at once with an AsyncOp; `data` may be
+        reused immediately. op.finish() -> (parity shares, B, padlen).
+        parity: optional caller-owned output arrays (n-k of >= B bytes;
+        page-locked ones are written in place by the kernel)."""
+        buf = _as_u8(data)
+        B = block_size(k, buf.size) if k else 0
+        p = max(n - k, 0)
+        outs = list(parity) if parity is not None else \
+            [np.zeros(max(B, 1), dtype=np.uint8) for _ in range(p)]
+        ptrs = (vp * max(p, 1))(*[o.ctypes.data for o in outs])
+        b, pad = sz(), sz()
+        op = AsyncOp(self, notify)
+        rc = lib().storb_rs_encode_async(self._h, k, n, buf.ctypes.data if buf.size else None,
+                                         buf.size, ptrs, C.byref(b), C.byref(pad), op._cb,
+                                         None, C.byref(op._h))
+        self._check(rc, "storb_rs_encode_async")
+        op._keep = outs
+        op._result = lambda: ([o[: b.value].tobytes() for o in outs], int(b.value),
+                              int(pad.value))
+        return op
+
+    def decode_async(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
+                     padlen: int, notify=None) -> "AsyncOp":
+        """storb_rs_decode_async; op.finish() -> the chunk bytes."""
+        arrs = [_as_u8(s) for s in shares]
+        ptrs = (vp * max(len(arrs), 1))(*[a.ctypes.data for a in arrs])
+        ids = (C.c_uint32 * max(len(idx), 1))(*idx)
+        outlen = max(k * block - padlen, 0)
+        out = np.zeros(max(outlen, 1), dtype=np.uint8)
+        op = AsyncOp(self, notify)
+        rc = lib().storb_rs_decode_async(self._h, k, n, ptrs, ids, len(arrs), block, padlen,
+                                         out.ctypes.data, op._cb, None, C.byref(op._h))
+        self._check(rc, "storb_rs_decode_async")
+        op._keep = out
+        op._result = lambda: out[:outlen].tobytes()
+        return op
+
     def repair(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
                targets: Sequence[int]) -> list[bytes]:
         """Regenerate shares `targets` (data or parity) of one stripe from the
@@ -468,6 +518,43 @@ class Context:
 
 
 _tls = threading.local()
+
+
+class AsyncOp:
+    """An in-flight storb_rs_*_async call: test() polls, finish() waits, writes
+    the outputs and returns the call's result (exactly once). `notify` (a
+    Python callable, optional) runs once when the device work is done, on a
+    HIP runtime thread."""
+
+    EAGAIN = 6
+
+    def __init__(self, ctx: Context, notify=None):
+        self._ctx = ctx  # keeps the context alive until finish
+        self._h = vp()
+        self._done = False
+        self._keep = None
+        self._result = None
+        self._notify = notify
+        self._cb = NOTIFY_FN(lambda _u: notify()) if notify else C.cast(None, NOTIFY_FN)
+
+    def test(self) -> bool:
+        if self._done:
+            return True
+        rc = lib().storb_rs_op_test(self._h)
+        if rc == self.EAGAIN:
+            return False
+        if rc != OK:
+            raise StorbRsError(rc, "storb_rs_op_test")
+        return True
+
+    def finish(self):
+        if self._done:
+            raise RuntimeError("op already finished")
+        self._done = True
+        rc = lib().storb_rs_op_finish(self._h)
+        if rc != OK:
+            raise StorbRsError(rc, "storb_rs_op_finish")
+        return self._result()
 
 
 def thread_context() -> Context:

@@ -9,6 +9,7 @@
 //                   repair): zero-copy and column-sliced paths
 //   host_batch.cpp  pipelined host batches (encode_chunks[_hashed],
 //                   decode_chunks)
+//   host_async.cpp  asynchronous single-chunk calls (start / test / finish)
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -96,6 +97,15 @@ struct Tables {
   }
 };
 
+// One in-flight asynchronous host call (host_async.cpp): its own stream,
+// completion event and page-locked staging, reused once the op is finished.
+struct AsyncSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  PinBuf in, out;
+  bool busy = false;
+};
+
 struct DeviceGuard {
   int prev = -1;
   bool ok = false;
@@ -135,6 +145,10 @@ struct storb_rs_ctx {
   // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
   bool zc_batch = true;
   hipEvent_t slice_ev[storb_rs::detail::kMaxSlices] = {};  // sliced single-call pipeline
+  // Slots of the asynchronous host calls (host_async.cpp); async_mu guards
+  // the busy flags, which finish() clears without holding mu.
+  std::mutex async_mu;
+  std::vector<std::unique_ptr<storb_rs::detail::AsyncSlot>> async_slots;
 };
 
 namespace storb_rs {

@@ -129,7 +129,7 @@ class Jit {
     if (it != entries_.end()) {
       e = it->second;
     } else {
-      if (entries_.size() >= max_kernels()) return nullptr;
+      if (entries_.size() >= max_kernels() || stop_) return nullptr;  // budget spent / exiting
       e = std::make_shared<Entry>();
       e->src = src();
       entries_.emplace(key, e);

@@ -486,6 +486,8 @@ const char *storb_rs_strerror(int code) {
     case STORB_RS_EDEVICE: return "HIP device error";
     case STORB_RS_ENOMEM: return "out of memory";
     case STORB_RS_ENODEV: return "no usable gfx950 device";
+    case STORB_RS_EAGAIN: return "async op still running";
+    case STORB_RS_EBUSY: return "too many unfinished async ops on the context";
     default: return "unknown error";
   }
 }
@@ -537,6 +539,11 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto &sl : ctx->async_slots) {  // unfinished async ops: their work ends here
+    (void)hipStreamSynchronize(sl->stream);
+    (void)hipStreamDestroy(sl->stream);
+    (void)hipEventDestroy(sl->done);
+  }
   delete ctx;  // frees tables, staging and pinned buffers on ctx->device
 }
 
