@@ -74,7 +74,11 @@ int acquire_slot(storb_rs_ctx *ctx, AsyncSlot **out) {
     return fail(ctx, STORB_RS_EBUSY, "too many unfinished async ops on this context");
   auto s = std::make_unique<AsyncSlot>();
   HIP_TRY(ctx, hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  HIP_TRY(ctx, hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+  const hipError_t e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    (void)hipStreamDestroy(s->stream);
+    return hip_fail(ctx, e, "hipEventCreateWithFlags(async slot)");
+  }
   s->busy = true;
   *out = s.get();
   ctx->async_slots.push_back(std::move(s));
