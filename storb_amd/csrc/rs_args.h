@@ -80,14 +80,23 @@ constexpr BsShape bs_shape(int K, int R) {
 }
 
 // Shares per load group (R x 8 accumulators + 2 x G x 8 loaded dwords + 30
-// table entries must fit): at k = 16 with up to 8 rows, 8 shares per group
+// table entries must fit): at k = 16 with 6-8 rows, 8 shares per group
 // (196 VGPRs) streams 2 % faster than 4 (141 VGPRs) -- both run 2 waves per
-// SIMD (tools/bstune.hip, profiles/r2_bstune.txt); 16 rows leave room for 2.
+// SIMD (tools/bstune.hip, profiles/r2_bstune.txt); with up to 5 rows (the
+// common decodes: a few miners lost) 4 per group in the two-wave
+// workgroups is 2-6 % faster than 8 at k = 16 and 32 (16 in + 2 out 193 ->
+// 183 us, + 4 out 223 -> 214; k = 32 + 4 out 194 -> 192;
+// profiles/r2_bstune_fewrows.txt); 16 rows leave room for 2.
 constexpr int bs_group(int K, int R) {
   return K <= 8 ? K
                 : (R >= 12 ? (K % 2 == 0 ? 2 : 1)
-                           : (R <= 8 && K % 8 == 0 ? 8 : (K % 4 == 0 ? 4 : (K % 2 == 0 ? 2 : 1))));
+                           : (R <= 5 && K % 4 == 0
+                                  ? 4
+                                  : (R <= 8 && K % 8 == 0
+                                         ? 8
+                                         : (K % 4 == 0 ? 4 : (K % 2 == 0 ? 2 : 1)))));
 }
+
 }  // namespace bs
 
 }  // namespace storb_rs

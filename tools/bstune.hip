@@ -85,11 +85,32 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec =
                     return bs::launch_bitslice<K, N>(a, s);
                   }, {}});
   constexpr int G = bs::bs_group(K, R);
-  add<K, N, G, 256, 0>(vs, {0, 2});
-  add<K, N, G, 128, 0>(vs, {3, 4});
-  add<K, N, G, 128, 1>(vs, {4});
-  add<K, N, G, 64, 0>(vs, {4, 5, 6, 8});
-  add<K, N, G, 64, 1>(vs, {4, 5, 6, 8});
+  if (std::getenv("BSTUNE_FEWROWS")) {  // decodes with few lost rows: G x (T, cap)
+    if constexpr (R <= 8) {
+      add<K, N, 2, 128, 0>(vs, {3});
+      add<K, N, 4, 128, 0>(vs, {3});
+      add<K, N, 8, 128, 0>(vs, {3});
+      add<K, N, 4, 64, 1>(vs, {5, 6});
+      add<K, N, 4, 64, 0>(vs, {5});
+      add<K, N, 4, 128, 1>(vs, {3});
+    }
+  } else if (std::getenv("BSTUNE_GROUPS")) {  // load-group size at the product shapes
+    add<K, N, G, 64, 1>(vs, {6});
+    add<K, N, G, 128, 0>(vs, {3, 4});
+    if constexpr (K == 16) {
+      add<K, N, 16, 64, 1>(vs, {4, 6, 8});
+      add<K, N, 16, 128, 0>(vs, {2, 3, 4});
+      add<K, N, 2, 64, 1>(vs, {6, 8});
+      add<K, N, 2, 128, 0>(vs, {3, 4});
+      add<K, N, 4, 128, 0>(vs, {3, 4});
+    }
+  } else {
+    add<K, N, G, 256, 0>(vs, {0, 2});
+    add<K, N, G, 128, 0>(vs, {3, 4});
+    add<K, N, G, 128, 1>(vs, {4});
+    add<K, N, G, 64, 0>(vs, {4, 5, 6, 8});
+    add<K, N, G, 64, 1>(vs, {4, 5, 6, 8});
+  }
   // parity region: Storb's n - k = k / 2 shares per stripe in the decode layout
   constexpr int P = K / 2;
   const uint64_t in_bytes = (uint64_t)nstripes * K * B, out_bytes = (uint64_t)nstripes * R * B;
@@ -158,7 +179,23 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec =
 
 int main(int argc, char **argv) {
   const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
-  const int which = argc > 2 ? std::atoi(argv[2]) : 0;  // 0 all, 1 encode, 2 decode
+  const int which = argc > 2 ? std::atoi(argv[2]) : 0;  // 0 all, 1 encode, 2 decode, 3 k=16 only
+  if (which == 4) {  // few-row decodes (BSTUNE_FEWROWS)
+    run<16, 18>("decode k=16, 2 lost (in place)", 128, 512 << 10, rounds, true);
+    run<16, 19>("decode k=16, 3 lost (in place)", 128, 512 << 10, rounds, true);
+    run<16, 20>("decode k=16, 4 lost (in place)", 128, 512 << 10, rounds, true);
+    run<16, 21>("decode k=16, 5 lost (in place)", 128, 512 << 10, rounds, true);
+    run<32, 34>("decode k=32, 2 lost (in place)", 32, 1 << 20, rounds, true);
+    run<32, 36>("decode k=32, 4 lost (in place)", 32, 1 << 20, rounds, true);
+    run<32, 40>("decode k=32, 8 lost (in place)", 32, 1 << 20, rounds, true);
+    return 0;
+  }
+  if (which == 3) {
+    run<16, 24>("RS(16,8) encode 128 x 8 MiB", 128, 512 << 10, rounds);
+    run<16, 18>("decode k=16, 2 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    run<16, 24>("decode k=16, 8 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    return 0;
+  }
   if (which != 2) {
     run<16, 24>("RS(16,8) encode 128 x 8 MiB", 128, 512 << 10, rounds);
     run<32, 48>("RS(32,16) encode 32 x 32 MiB", 32, 1 << 20, rounds);
