@@ -22,7 +22,9 @@ Other BASELINE configs (not the driver's line):
               (strong scaling: total work fixed)
   --config 5  RS(16,8) [storb k=16,m=24]: 128 x 8 MiB chunks (a 1 GiB object)
   --config 6  RS(32,16) [storb k=32,m=48]: 32 x 32 MiB chunks
-              (5/6: --erase E loses data shares 0..E-1 for the decode leg)
+  --config 7  RS(64,32) [storb k=64,m=96]: 8 x 128 MiB chunks (Storb's sizing of
+              objects from ~160 GiB up, piece.rs:292-317)
+              (5/6/7: --erase E loses data shares 0..E-1 for the decode leg)
 
 Launch: python bench.py [--gpus N --steps K --warmup W]. One rank per GPU:
 under torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE env, which must agree
@@ -58,7 +60,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--config", type=int, choices=[2, 3, 4, 5, 6], default=2,
+    p.add_argument("--config", type=int, choices=[2, 3, 4, 5, 6, 7], default=2,
                    help="BASELINE config; 5 = the device-resident GPU half of config 5 "
                         "(1 GiB object -> 128 x 8 MiB chunks, storb k=16, m=24); 6 = "
                         "Storb's widest geometry (32 MiB chunks of 16-64 GiB objects, "
@@ -424,9 +426,11 @@ def leg_kernel_match(a, w, leg):
     if leg == "encode":
         if a.kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48)):
             return f"rs_encode_bitslice<{w.k}, {w.n}>"
+        if "encode" in w.jit_legs:
+            return "storb_bs_jit"
         k, r = w.k, w.n - w.k
     else:
-        if w.jit_decode:
+        if "decode" in w.jit_legs:
             return "storb_bs_jit"
         k, r = w.k, sum(1 for x in w.erased if x < w.k)
     kb = 1
@@ -506,10 +510,12 @@ def kernel_names(kernel, w):
     if "encode" in w.legs:
         bits = kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48))
         names["encode"] = (f"rs_encode_bitslice<{w.k},{w.n}>" if bits
+                           else f"storb_bs_jit<{w.k},{w.n - w.k}> (hipRTC)"
+                           if "encode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")
     if "decode" in w.legs:
         e = sum(1 for x in w.erased if x < w.k)
-        names["decode"] = (f"storb_bs_jit<{w.k},{e}> (hipRTC)" if w.jit_decode
+        names["decode"] = (f"storb_bs_jit<{w.k},{e}> (hipRTC)" if "decode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{e}>")
     return names
 
@@ -539,7 +545,7 @@ class Workload:
             self.scaling = "weak"
             self.workload = (f"RS(k=8,m=4) [storb k=8,m=12] decode, erased [0, 3, 5], "
                              f"survivors first 8 by index, {N} x 256 KiB chunks per GPU")
-        elif c in (5, 6):
+        elif c in (5, 6, 7):
             E = 2 if a.erase is None else a.erase
             if c == 5:
                 self.k, self.n, chunk = 16, 24, 8 << 20
@@ -547,12 +553,18 @@ class Workload:
                 what = "8 MiB chunks (a 1 GiB object)"
                 self.metric = ("GiB/s device-resident RS encode+decode, 8 MiB chunks k=16 m=8 "
                                "(Storb's geometry for a 1 GiB object)")
-            else:
+            elif c == 6:
                 self.k, self.n, chunk = 32, 48, 32 << 20
                 N = a.chunks or 32
                 what = "32 MiB chunks (objects of 16-64 GiB)"
                 self.metric = ("GiB/s device-resident RS encode+decode, 32 MiB chunks k=32 m=16 "
-                               "(Storb's widest geometry)")
+                               "(Storb's geometry for objects of 16 GiB to ~160 GiB)")
+            else:
+                self.k, self.n, chunk = 64, 96, 128 << 20
+                N = a.chunks or 8
+                what = "128 MiB chunks (objects from ~160 GiB)"
+                self.metric = ("GiB/s device-resident RS encode+decode, 128 MiB chunks k=64 m=32 "
+                               "(Storb's widest geometry, objects from ~160 GiB)")
             if not 0 < E <= self.n - self.k:
                 raise SystemExit(f"--erase must be in 1..{self.n - self.k}")
             self.erased = list(range(E))
@@ -575,7 +587,7 @@ class Workload:
             self.workload = (f"{a.objects} x 1 MiB objects, object i on rank i mod {world}; "
                              f"this rank {N} objects, one batched launch per step")
         self.chunk, self.N = chunk, N
-        self.jit_decode = False
+        self.jit_legs = set()  # legs whose launches are run-time-compiled kernels
         k, n = self.k, self.n
         self.B = chunk // k
         self.survivors = [i for i in range(n) if i not in self.erased][:k]
@@ -680,10 +692,19 @@ def main():
     # A decode matrix the table kernel is VALU-bound on gets its own compiled
     # bit-sliced kernel (rs_jit.cpp); the first decode queued its compile.
     # Let it finish so the timed steps run what a steady-state download runs.
-    if "decode" in w.legs:
-        w.decode()
+    # (Config 7's k = 64 encode runs compiled kernels too.) One pass of every
+    # leg queues them; wait for the compiles.
+    for leg in w.legs:
+        getattr(w, leg)()
+    stream.synchronize()
+    _lib.jit_wait()
+    # Which legs run compiled kernels (for the kernel names and the PMC match).
+    for leg in w.legs:
+        j0 = _lib.jit_stats()["launches"]
+        getattr(w, leg)()
         stream.synchronize()
-        _lib.jit_wait()
+        if _lib.jit_stats()["launches"] > j0:
+            w.jit_legs.add(leg)
     jit0 = _lib.jit_stats()
     legs = [getattr(w, leg) for leg in w.legs]
     for _ in range(a.warmup):
@@ -719,7 +740,6 @@ def main():
     elapsed = time.perf_counter() - t0
     gpu_ms = e_start.elapsed_time(e_end) / a.steps
     jit1 = _lib.jit_stats()
-    w.jit_decode = jit1["launches"] - jit0["launches"] >= a.steps + a.warmup
     if not each:
         # Per-leg split (which kernel took what) from an untimed pass of the
         # same steps with an event after every leg; reported, not used for
@@ -797,7 +817,10 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.minimal:
-        if not a.no_traffic:
+        if not a.no_traffic and a.config == 7:
+            out["roofline"]["traffic_source"] = (
+                "not measured: config 7's legs are several compiled launches each (row blocks)")
+        elif not a.no_traffic:
             pmc = pmc_traffic(a, w)
             out["roofline"].update(pmc)
         out["roofline"]["copy_ceiling_gbs"] = copy_ceiling(ctx, dev, stream)

@@ -228,7 +228,8 @@ int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant);
 /* Run-time-compiled bit-sliced kernels. Decode and repair apply rows of the
  * inverted survivor matrix, known only when the erasure pattern is. Under
  * AUTO, a matrix the table kernel is measured slower on (k >= 12 with >= 2
- * rows, k = 8..11 with >= 6; batches >= 4 MiB)
+ * rows, k = 8..11 with >= 6, k <= 64, up to 32 rows as launches of <= 16;
+ * batches >= 4 MiB)
  * gets its own bit-sliced kernel, compiled with hipRTC on a background thread
  * and cached for the process; calls made while it compiles run the table
  * kernel. STORB_RS_JIT=0 disables, =sync compiles before the first launch;

@@ -20,17 +20,22 @@ struct PermTab;  // gf256.hpp (host side only)
 
 // One launch applies a (r x k) coefficient block to k input share slots and
 // writes (or XOR-accumulates into) r output share slots, for every stripe.
-// Larger matrices are tiled over several launches by the host (storb_rs.cpp).
+// Larger matrices are tiled over several launches by the host (storb_rs.cpp):
+// the table kernels take up to kSlotK inputs per launch, the bit-sliced ones
+// kMaxIn -- Storb sizes the chunks of objects from ~160 GiB up (128-256 MiB)
+// k = 64 (piece.rs:292-317), and a launch that sees every input writes each
+// output once instead of XOR-accumulating it over column tiles.
 constexpr int kSlotK = 32;
 constexpr int kSlotR = 16;
+constexpr int kMaxIn = 64;
 
 // Largest k bucket with COPY instantiations of the table kernel; wider
 // decodes copy survivors with hipMemcpy2DAsync before the kernel.
 constexpr uint32_t kCopyMaxK = 16;
 
 struct ApplyArgs {
-  const uint8_t *in[kSlotK];
-  uint64_t in_stride[kSlotK];
+  const uint8_t *in[kMaxIn];
+  uint64_t in_stride[kMaxIn];
   uint8_t *out[kSlotR];
   uint64_t out_stride[kSlotR];
   const PermTab *ptab;  // nibble tables [col][tab_rows], rows >= r zeroed
@@ -44,8 +49,8 @@ struct ApplyArgs {
   // also stored, as loaded, to copy[j] (null = not copied). ncopy > 0 selects
   // the COPY kernels; r may then be 0 (pure assembly).
   uint32_t ncopy;
-  uint8_t *copy[kSlotK];
-  uint64_t copy_stride[kSlotK];
+  uint8_t *copy[kMaxIn];
+  uint64_t copy_stride[kMaxIn];
 };
 
 // Launch shape of the bit-sliced kernels (rs_bitslice_core.h), shared by
@@ -56,7 +61,6 @@ struct ApplyArgs {
 namespace bs {
 constexpr int kBsThreads = 256;
 constexpr unsigned bs_cols_per_tile(int threads) { return 2u * static_cast<unsigned>(threads); }
-constexpr unsigned kBsColsPerTile = bs_cols_per_tile(kBsThreads);
 
 // Launch shape per (k, rows), from the sweep of workgroup size x tile
 // rotation x resident-workgroup cap: over the kernels alone

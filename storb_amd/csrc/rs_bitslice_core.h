@@ -179,10 +179,14 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
     for (int b = 0; b < 8; b++) acc[p][b] = 0;
 
   v4 buf[2][G][2];
-  const uint32_t ca = v0 < cols ? v0 : cols - 1, cb = v0 + 64 < cols ? v0 + 64 : cols - 1;
+  uint32_t ca = v0 < cols ? v0 : cols - 1, cb = v0 + 64 < cols ? v0 + 64 : cols - 1;
   load_group<G>(a, 0, stripe, ca, cb, buf[0]);
   static_for<K / G>([&](auto GI) {
     constexpr int gi = decltype(GI)::value;
+    // k > 32: the load addresses pass through an ordering point, so group
+    // gi + 1's loads cannot be hoisted above group gi - 1's fold (with 32+
+    // groups the scheduler otherwise ran many groups ahead and spilled).
+    if constexpr (K > 32) asm volatile("" : "+v"(ca), "+v"(cb));
     if constexpr (gi + 1 < K / G)
       load_group<G>(a, (gi + 1) * G, stripe, ca, cb, buf[(gi + 1) & 1]);
     static_for<G>([&](auto GG) {

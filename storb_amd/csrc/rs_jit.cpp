@@ -361,9 +361,7 @@ bool enabled() { return mode() != Mode::Off; }
 // with r >= 6 is the VALU model's guess (~5.5 ops per HBM byte), not
 // measured. Only for batches large enough to matter (>= 4 MiB).
 static bool valu_bound(uint32_t k, uint32_t rows) {
-  if (k < 8 || k > static_cast<uint32_t>(kSlotK) || rows == 0 ||
-      rows > static_cast<uint32_t>(kSlotR))
-    return false;
+  if (k < 8 || k > static_cast<uint32_t>(kMaxIn) || rows == 0 || rows > kMaxRows) return false;
   const uint32_t min_rows = k >= 12 ? 2 : 6;
   return always() || rows >= min_rows;
 }
@@ -391,45 +389,99 @@ static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *c
   return e;
 }
 
-hipError_t try_launch(int device, const ApplyArgs &a, const uint8_t *coef, hipStream_t s,
+// Row blocks of at most kSlotR rows (the accumulators of one launch), as
+// even as possible: 20 rows -> 10 + 10. Block b covers rows [r0(b), r0(b+1)).
+static uint32_t row_blocks(uint32_t rows) { return (rows + kSlotR - 1) / kSlotR; }
+static uint32_t row_start(uint32_t rows, uint32_t b) {
+  const uint32_t nb = row_blocks(rows);
+  return static_cast<uint32_t>(static_cast<uint64_t>(rows) * b / nb);
+}
+
+hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
+                      const size_t *out_stride, const uint8_t *coef, hipStream_t s,
                       bool *launched) {
   *launched = false;
-  if (a.k == 0 || a.k > static_cast<uint32_t>(kSlotK) || a.r == 0 ||
-      a.r > static_cast<uint32_t>(kSlotR) || a.accumulate || !vector_ok(a))
+  if (a.k == 0 || a.k > static_cast<uint32_t>(kMaxIn) || a.r == 0 || a.r > kMaxRows ||
+      a.accumulate)
     return hipSuccess;
+  {  // 16-B aligned slots (the dwordx4 kernels); outputs come from d_out
+    ApplyArgs in_only = a;
+    in_only.r = 0;
+    if (!vector_ok(in_only)) return hipSuccess;
+    for (uint32_t i = 0; i < a.r; i++)
+      if ((reinterpret_cast<uintptr_t>(d_out[i]) | out_stride[i]) % 16) return hipSuccess;
+  }
   const uint64_t cols = a.block >> 4;
-  const bs::BsShape sh = shape(a.k, a.r);
-  const uint64_t cpt = bs::bs_cols_per_tile(sh.threads);
-  const uint64_t blocks = ((cols + cpt - 1) / cpt) * a.nstripes;
-  if (blocks == 0 || blocks > 0x7FFFFFFFull) return hipSuccess;  // table kernel handles it
+  if (cols == 0 || (cols + 127) / 128 * a.nstripes > 0x7FFFFFFFull) return hipSuccess;
   uint64_t copy_mask = 0;
   for (uint32_t j = 0; a.ncopy && j < a.k; j++)
     if (a.copy[j]) copy_mask |= 1ull << j;
+  // Every row block's kernel must be ready (all or none: a matrix is never
+  // split between the compiled and the table kernels); the first block
+  // also does the fused-assembly copies.
   Jit &J = jit();
-  auto e = entry_for(a.k, a.r, coef, copy_mask, false);
-  if (!e || e->state != Entry::Ready) {
+  const uint32_t nb = row_blocks(a.r);
+  std::vector<std::shared_ptr<Entry>> es(nb);
+  bool ready = true;
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t r0 = row_start(a.r, b), rr = row_start(a.r, b + 1) - r0;
+    es[b] = entry_for(a.k, rr, coef + static_cast<size_t>(r0) * a.k, b == 0 ? copy_mask : 0,
+                      false);
+    ready = ready && es[b] && es[b]->state == Entry::Ready;
+  }
+  if (!ready) {
     J.fallbacks++;
     return hipSuccess;
   }
-  hipFunction_t f = nullptr;
-  hipError_t r = J.function(*e, device, &f);
+  std::vector<hipFunction_t> fs(nb);
+  for (uint32_t b = 0; b < nb; b++) {
+    hipError_t r = J.function(*es[b], device, &fs[b]);
+    if (r != hipSuccess) return r;
+  }
+  // One launch per row block, each over the whole batch: a.r rows in nb > 1
+  // blocks read every input nb times. (Going block after block over ranges
+  // small enough for the later blocks to re-read the inputs from the 256 MiB
+  // Infinity Cache measured slower -- 0.49 -> 0.77 ms at 128 MiB ranges --
+  // as a k = 64 range that fits leaves too few workgroups per launch;
+  // profiles/r2_k64/.)
+  hipError_t r = hipSuccess;
+  for (uint32_t b = 0; b < nb && r == hipSuccess; b++) {
+    const uint32_t r0 = row_start(a.r, b), rr = row_start(a.r, b + 1) - r0;
+    const bs::BsShape sh = shape(a.k, rr);
+    const uint64_t cpt = bs::bs_cols_per_tile(sh.threads);
+    const uint64_t blocks = ((cols + cpt - 1) / cpt) * a.nstripes;
+    if (blocks == 0 || blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ApplyArgs arg = a;
+    arg.r = rr;
+    if (b > 0) {
+      arg.ncopy = 0;
+      for (uint32_t j = 0; j < a.k; j++) arg.copy[j] = nullptr;
+    }
+    for (uint32_t i = 0; i < rr; i++) {
+      arg.out[i] = d_out[r0 + i];
+      arg.out_stride[i] = out_stride[r0 + i];
+    }
+    void *params[] = {&arg};
+    r = hipModuleLaunchKernel(fs[b], static_cast<unsigned>(blocks), 1, 1,
+                              static_cast<unsigned>(sh.threads), 1, 1, 0, s, params, nullptr);
+    if (r == hipSuccess) J.launches++;
+  }
   if (r != hipSuccess) return r;
-  ApplyArgs arg = a;
-  void *params[] = {&arg};
-  r = hipModuleLaunchKernel(f, static_cast<unsigned>(blocks), 1, 1,
-                            static_cast<unsigned>(sh.threads), 1, 1, 0, s,
-                            params, nullptr);
-  if (r != hipSuccess) return r;
-  J.launches++;
   *launched = true;
   return hipSuccess;
 }
 
 int prepare(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask, bool wait) {
   if (!enabled() || !valu_bound(k, rows)) return 0;
-  auto e = entry_for(k, rows, coef, copy_mask, wait);
-  if (!e) return 0;
-  return e->state == Entry::Ready ? 1 : (e->state == Entry::Failed ? -1 : 0);
+  int res = 1;
+  for (uint32_t b = 0; b < row_blocks(rows); b++) {
+    const uint32_t r0 = row_start(rows, b), rr = row_start(rows, b + 1) - r0;
+    auto e = entry_for(k, rr, coef + static_cast<size_t>(r0) * k, b == 0 ? copy_mask : 0, wait);
+    if (!e) return 0;
+    if (e->state == Entry::Failed) return -1;
+    if (e->state != Entry::Ready) res = 0;
+  }
+  return res;
 }
 
 }  // namespace jit

@@ -11,16 +11,23 @@
 namespace storb_rs {
 namespace jit {
 
+// Rows one compiled matrix may have: split into launches of <= kSlotR rows
+// (Storb's k = 64 geometry has 32 parity rows).
+constexpr uint32_t kMaxRows = 2 * kSlotR;
+
 // STORB_RS_JIT != 0 (default on; "sync" compiles before the first launch).
 bool enabled();
 // Whether a (rows x k) matrix moving `bytes` per call is worth a compiled
 // kernel (the table kernel measured slower on it, rs_jit.cpp).
 bool wanted(uint32_t k, uint32_t rows, uint64_t bytes);
-// Launch the compiled kernel of matrix `coef` (a.r x a.k, row-major) with
-// a's slots (a.copy[j] != null with a.ncopy: fused assembly) on stream s if
-// it is ready; queues its compilation otherwise. *launched = false means the
+// Launch the compiled kernel(s) of matrix `coef` (a.r x a.k, row-major, k <=
+// kMaxIn, r <= kMaxRows in row blocks of <= kSlotR) with a's input slots
+// (a.copy[j] != null with a.ncopy: fused assembly) and the a.r outputs
+// d_out / out_stride (a.out is not read) on stream s if every block is
+// ready; queues their compilation otherwise. *launched = false means the
 // caller runs the table kernel. `device` must be current.
-hipError_t try_launch(int device, const ApplyArgs &a, const uint8_t *coef, hipStream_t s,
+hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
+                      const size_t *out_stride, const uint8_t *coef, hipStream_t s,
                       bool *launched);
 
 // Queue the compile of matrix `coef` (rows x k) with the given copy mask,

@@ -235,8 +235,8 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
     copy = nullptr;
     if (rows == 0) return STORB_RS_OK;
   }
-  if (rows > 0 && ctx->variant == STORB_RS_KERNEL_AUTO && k <= static_cast<uint32_t>(kSlotK) &&
-      rows <= static_cast<uint32_t>(kSlotR) &&
+  if (rows > 0 && ctx->variant == STORB_RS_KERNEL_AUTO && k <= static_cast<uint32_t>(kMaxIn) &&
+      rows <= jit::kMaxRows &&
       jit::wanted(k, rows, static_cast<uint64_t>(k + rows) * block * nstripes)) {
     ApplyArgs a{};
     a.k = k;
@@ -250,14 +250,10 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
         a.ncopy++;
       }
     }
-    for (uint32_t i = 0; i < rows; i++) {
-      a.out[i] = d_out[i];
-      a.out_stride[i] = out_stride[i];
-    }
     a.block = block;
     a.nstripes = nstripes;
     bool launched = false;
-    HIP_TRY(ctx, jit::try_launch(ctx->device, a, coef, s, &launched));
+    HIP_TRY(ctx, jit::try_launch(ctx->device, a, d_out, out_stride, coef, s, &launched));
     if (launched) return STORB_RS_OK;
   }
   if (copy && !copy_fusable_table(ctx, k, block, d_in, in_stride, copy, copy_stride)) {

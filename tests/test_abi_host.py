@@ -118,9 +118,12 @@ def test_jit_compiles_decode_kernels_without_gpu():
     _lib.jit_prepare_decode(16, 24, [1, 2, 3, 5, 8, 13, 16, 17, 18, 19, 20, 21, 22, 23, 4, 6],
                             assemble=True)
     _lib.jit_prepare_decode(32, 48, list(range(16, 48)))
+    # k > 32 (Storb's k = 64 for objects from ~160 GiB; a short last chunk
+    # any k up to 64): one launch sees every input
+    _lib.jit_prepare_decode(40, 60, [x for x in range(60) if x not in (1, 7, 30)])
     st = _lib.jit_stats()
     assert st["failed"] == 0 and st["pending"] == 0
-    assert st["compiled"] == before["compiled"] + 3
+    assert st["compiled"] == before["compiled"] + 4
     # the same pattern again is a cache hit
     _lib.jit_prepare_decode(16, 24, list(range(8, 24)))
     assert _lib.jit_stats()["compiled"] == st["compiled"]

@@ -176,3 +176,39 @@ def test_jit_not_used_where_table_kernel_is_hbm_bound(ctx):
         st["compiled"] + st["pending"] + st["failed"]
     assert np.array_equal(data.cpu().numpy(), data_h)
     assert np.array_equal(d16g.cpu().numpy(), d16)
+
+
+@pytest.mark.timeout(600)
+def test_jit_k64_encode_and_decode(ctx):
+    """Storb's widest geometry: objects from ~160 GiB are chunked at 128-256
+    MiB and sized k = 64, m = 96 (piece.rs:292-317). Encode (32 parity rows)
+    and a 20-lost decode (20 rows) each run as two compiled launches of <= 16
+    rows that see all 64 inputs; an odd k = 40 decode too. Oracle-exact; the
+    compiles (several seconds each at k = 64) are waited for first."""
+    for k, n, B, ns, erased in [(64, 96, 16 << 10, 4, list(range(20))),
+                                (40, 60, 32 << 10, 4, [0, 3, 33])]:
+        data_h, par_h = oracle_batch(k, n, B, ns, 64 + k)
+        data = torch.from_numpy(data_h).to(DEV)
+        par = torch.zeros(ns * (n - k) * B, dtype=torch.uint8, device=DEV)
+        ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())  # queues compiles
+        surv = [i for i in range(n) if i not in erased]
+        _lib.jit_prepare_decode(k, n, surv, wait=True)
+        _lib.jit_wait()
+        torch.cuda.synchronize()
+        assert np.array_equal(par.cpu().numpy(), par_h), (k, "table-kernel encode")
+        par.zero_()
+        before = launches()
+        ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
+        torch.cuda.synchronize()
+        blocks = -(-(n - k) // 16)
+        assert launches() == before + blocks, "compiled encode did not run"
+        assert np.array_equal(par.cpu().numpy(), par_h), (k, "compiled encode")
+        view = data.view(ns, k, B)
+        for e in erased:
+            view[:, e].fill_(0xA5)
+        before = launches()
+        ctx.decode_batch_dev(k, n, B, ns, surv, data.data_ptr(), par.data_ptr(), data.data_ptr())
+        torch.cuda.synchronize()
+        assert launches() == before + -(-len(erased) // 16), "compiled decode did not run"
+        assert np.array_equal(data.cpu().numpy(), data_h), (k, "compiled decode")
+
