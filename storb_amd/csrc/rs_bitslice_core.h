@@ -97,7 +97,18 @@ __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-__device__ __forceinline__ v4 ld_nt(const v4 *p) { return __builtin_nontemporal_load(p); }
+// Loads: non-temporal (shares are read once) unless STORB_BS_LOAD_NT=0
+// (tools/k64pair.hip: whether cached loads let a second reader hit).
+#ifndef STORB_BS_LOAD_NT
+#define STORB_BS_LOAD_NT 1
+#endif
+__device__ __forceinline__ v4 ld_nt(const v4 *p) {
+#if STORB_BS_LOAD_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 // Stores: non-temporal unless STORB_RS_NT_STORES=0 (shares are touched once;
 // nt stores measured 5-9 % faster in steady state, profiles/r1_store_policy.txt).
 __device__ __forceinline__ void st_nt(v4 *p, v4 v) {
@@ -168,8 +179,9 @@ __device__ __forceinline__ void fence_acc(uint32_t (&acc)[R][8]) {
 // every byte in its own bit position, so the garbage never reaches a stored
 // byte -- one branch-free body for full and partial tiles.
 template <class M, int G>
-__device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uint32_t v0,
-                                        uint32_t cols) {
+__device__ __forceinline__ void bs_tile_to(const ApplyArgs &a, uint8_t *const *outp,
+                                           const uint64_t *out_stride, uint32_t stripe,
+                                           uint32_t v0, uint32_t cols) {
   constexpr int K = M::K, R = M::R;
   static_assert(K % G == 0, "group size must divide k");
   uint32_t acc[R][8];
@@ -212,12 +224,18 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
 #pragma unroll
   for (int p = 0; p < R; p++) {
     transpose8(acc[p]);
-    v4 *q = reinterpret_cast<v4 *>(a.out[p] + static_cast<uint64_t>(stripe) * a.out_stride[p]);
+    v4 *q = reinterpret_cast<v4 *>(outp[p] + static_cast<uint64_t>(stripe) * out_stride[p]);
     const v4 A = {acc[p][0], acc[p][1], acc[p][2], acc[p][3]};
     const v4 Bv = {acc[p][4], acc[p][5], acc[p][6], acc[p][7]};
     if (v0 < cols) st_nt(q + v0, A);
     if (v0 + 64 < cols) st_nt(q + v0 + 64, Bv);
   }
+}
+
+template <class M, int G>
+__device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uint32_t v0,
+                                        uint32_t cols) {
+  bs_tile_to<M, G>(a, a.out, a.out_stride, stripe, v0, cols);
 }
 
 // Grid: nstripes x tiles of bs_cols_per_tile(T) 16-B columns (rs_args.h);
