@@ -212,3 +212,29 @@ def test_jit_k64_encode_and_decode(ctx):
         assert launches() == before + -(-len(erased) // 16), "compiled decode did not run"
         assert np.array_equal(data.cpu().numpy(), data_h), (k, "compiled decode")
 
+
+
+@pytest.mark.timeout(600)
+def test_jit_k64_decode_into_separate_buffer(ctx):
+    """k = 64 decode into a fresh chunk buffer (decode_chunk semantics,
+    piece.rs:363-387): the first row block's kernel also stores every
+    surviving data share to its slot (fused assembly, a 64-bit copy mask);
+    20 lost rows = two compiled launches. Oracle-exact, sources untouched."""
+    k, n, B, ns = 64, 96, 16 << 10, 4
+    erased = [0, 5, 9, 13, 17, 21, 25, 29, 33, 37, 41, 45, 49, 53, 57, 61, 62, 63, 1, 2]
+    data_h, par_h = oracle_batch(k, n, B, ns, 6464)
+    surv = [i for i in range(n) if i not in erased]
+    _lib.jit_prepare_decode(k, n, surv, assemble=True, wait=True)
+    data = torch.from_numpy(data_h).to(DEV)
+    par = torch.from_numpy(par_h).to(DEV)
+    view = data.view(ns, k, B)
+    for e in erased:
+        view[:, e].fill_(0xA5)
+    out = torch.full_like(data, 0x5A)
+    before = launches()
+    ctx.decode_batch_dev(k, n, B, ns, surv, data.data_ptr(), par.data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    assert launches() == before + 2
+    assert np.array_equal(out.cpu().numpy(), data_h)
+    for e in erased:
+        assert bool((view[:, e] == 0xA5).all())
