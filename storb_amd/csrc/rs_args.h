@@ -27,7 +27,10 @@ struct PermTab;  // gf256.hpp (host side only)
 // output once instead of XOR-accumulating it over column tiles.
 constexpr int kSlotK = 32;
 constexpr int kSlotR = 16;
-constexpr int kMaxIn = 64;
+#ifndef STORB_RS_MAX_IN
+#define STORB_RS_MAX_IN 64  // (tools: -DSTORB_RS_MAX_IN=32 for a kernel-argument-size A/B)
+#endif
+constexpr int kMaxIn = STORB_RS_MAX_IN;
 
 // Largest k bucket with COPY instantiations of the table kernel; wider
 // decodes copy survivors with hipMemcpy2DAsync before the kernel.
