@@ -421,17 +421,29 @@ def config4_storb_faithful(ctx, w, stream, reps=5):
                     "chunks, k=2, m=3, one batched launch; bytes = k*B read + (n-k)*B written"}
 
 
+def leg_rows(w, leg):
+    """Rows of the matrix a leg applies: parity rows (encode) or lost data
+    shares (decode)."""
+    return w.n - w.k if leg == "encode" else sum(1 for x in w.erased if x < w.k)
+
+
+def jit_blocks(rows):
+    """Compiled launches of a rows-row matrix (rs_jit.cpp: row blocks of <= 16,
+    balanced) and the first block's rows."""
+    nb = -(-rows // 16)
+    return nb, rows // nb
+
+
 def leg_kernel_match(a, w, leg):
-    """Substring of the rocprofv3 kernel name each leg launches."""
+    """Substring of the rocprofv3 kernel name each leg launches (compiled
+    kernels are named storb_bs_jit_k<k>_r<rows>_{ip,asm}, rs_jit.cpp)."""
+    if leg in w.jit_legs:
+        return f"storb_bs_jit_k{w.k}_r{jit_blocks(leg_rows(w, leg))[1]}_"
     if leg == "encode":
         if a.kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48)):
             return f"rs_encode_bitslice<{w.k}, {w.n}>"
-        if "encode" in w.jit_legs:
-            return "storb_bs_jit"
         k, r = w.k, w.n - w.k
     else:
-        if "decode" in w.jit_legs:
-            return "storb_bs_jit"
         k, r = w.k, sum(1 for x in w.erased if x < w.k)
     kb = 1
     while kb < min(k, 32):
@@ -503,6 +515,12 @@ def pmc_traffic(a, w):
                                f" s); read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE")}
 
 
+def jit_name(w, leg):
+    nb, r0 = jit_blocks(leg_rows(w, leg))
+    return (f"storb_bs_jit_k{w.k}_r{r0}_* (hipRTC)"
+            + (f" x {nb} row blocks" if nb > 1 else ""))
+
+
 def kernel_names(kernel, w):
     """The kernels the legs launch (rs_bitslice.hpp / rs_device.hpp)."""
     names = {}
@@ -510,12 +528,11 @@ def kernel_names(kernel, w):
     if "encode" in w.legs:
         bits = kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48))
         names["encode"] = (f"rs_encode_bitslice<{w.k},{w.n}>" if bits
-                           else f"storb_bs_jit<{w.k},{w.n - w.k}> (hipRTC)"
-                           if "encode" in w.jit_legs
+                           else jit_name(w, "encode") if "encode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")
     if "decode" in w.legs:
         e = sum(1 for x in w.erased if x < w.k)
-        names["decode"] = (f"storb_bs_jit<{w.k},{e}> (hipRTC)" if "decode" in w.jit_legs
+        names["decode"] = (jit_name(w, "decode") if "decode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{e}>")
     return names
 
@@ -809,6 +826,9 @@ def main():
             "leg_ms_source": ("events after every leg inside the timed region" if each else
                               "separate untimed pass with an event after every leg"),
             "alg_bytes_per_launch": alg,
+            "kernel_match": {leg: leg_kernel_match(a, w, leg) for leg in w.legs},
+            "launches_per_leg": {leg: jit_blocks(leg_rows(w, leg))[0] if leg in w.jit_legs
+                                 else 1 for leg in w.legs},
             "copy_ceiling_gbs": None,
             "jit": {"launches_in_run": jit1["launches"] - jit0["launches"],
                     "compiled": jit1["compiled"], "compile_ms": round(jit1["compile_ms"], 1),

@@ -58,13 +58,15 @@ def main():
         rows = list(csv.DictReader(open(stats[0])))
         legs = {}
         for leg, ms in line["roofline"]["leg_ms"].items():
-            sub = kernel_match(line, leg)
+            sub = (line["roofline"].get("kernel_match") or {}).get(leg) or kernel_match(line, leg)
+            per_leg = (line["roofline"].get("launches_per_leg") or {}).get(leg, 1)
             hit = [r for r in rows if sub in r["Name"]]
             if not hit:
                 legs[leg] = {"kernel": sub, "trace": None}
                 continue
             r = max(hit, key=lambda x: int(x["Calls"]))
-            avg_ms = float(r["AverageNs"]) / 1e6
+            # a leg of several launches (row blocks of a compiled matrix)
+            avg_ms = float(r["AverageNs"]) / 1e6 * per_leg
             alg = line["roofline"]["alg_bytes_per_launch"][leg]
             legs[leg] = {"kernel": r["Name"], "calls": int(r["Calls"]),
                          "trace_avg_ms": round(avg_ms, 4), "bench_leg_ms": ms,

@@ -79,6 +79,7 @@ struct Entry {
   enum State { Pending, Ready, Failed };
   std::atomic<State> state{Pending};  // read by launching threads without the lock
   std::string src;
+  std::string name;  // kernel symbol: storb_bs_jit_k<k>_r<rows>_{ip,asm}
   std::vector<char> code;
   std::string log;
   std::map<int, hipFunction_t> fn;  // per device
@@ -119,10 +120,10 @@ class Jit {
   }
 
   // The entry for key, created and queued for compilation if new (nullptr
-  // when the kernel budget is spent); src() writes the kernel source, only
-  // for a new entry. In Sync mode waits for the compile.
+  // when the kernel budget is spent); src() writes the kernel source (symbol
+  // `name`), only for a new entry. In Sync mode waits for the compile.
   template <typename Src>
-  std::shared_ptr<Entry> get(const std::string &key, Src &&src) {
+  std::shared_ptr<Entry> get(const std::string &key, const std::string &name, Src &&src) {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = entries_.find(key);
     std::shared_ptr<Entry> e;
@@ -132,6 +133,7 @@ class Jit {
       if (entries_.size() >= max_kernels() || stop_) return nullptr;  // budget spent / exiting
       e = std::make_shared<Entry>();
       e->src = src();
+      e->name = name;
       entries_.emplace(key, e);
       queue_.push_back(e);
       pending_++;
@@ -157,7 +159,7 @@ class Jit {
     hipModule_t m = nullptr;
     hipError_t r = hipModuleLoadData(&m, e.code.data());
     if (r != hipSuccess) return r;
-    r = hipModuleGetFunction(f, m, "storb_bs_jit");
+    r = hipModuleGetFunction(f, m, e.name.c_str());
     if (r != hipSuccess) return r;
     e.modules.push_back(m);
     e.fn[device] = *f;
@@ -301,6 +303,13 @@ bs::BsShape shape(uint32_t k, uint32_t r) {
   return s;
 }
 
+// Kernel symbol, so profiles tell the compiled kernels apart (bench.py and
+// profiles/summarize.py match on the "storb_bs_jit_k<k>_r<rows>_" prefix).
+std::string kernel_name(uint32_t k, uint32_t rows, uint64_t copy_mask) {
+  return "storb_bs_jit_k" + std::to_string(k) + "_r" + std::to_string(rows) +
+         (copy_mask ? "_asm" : "_ip");
+}
+
 // The kernel source for a (rows x k) matrix: bit b' of row[p][j][b] is bit b
 // of coef[p][j] * 2^b' (the GF(2) matrix of multiplication by coef[p][j]).
 std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask,
@@ -332,8 +341,8 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
   // 2 waves per SIMD (<= 256 registers): without the hint, 64- and 128-lane
   // workgroups let the allocator take 257 at k = 32 (1 wave per SIMD)
   s += "extern \"C\" __global__ __launch_bounds__(" + std::to_string(sh.threads) +
-       ") __attribute__((amdgpu_waves_per_eu(2))) void storb_bs_jit(const storb_rs::ApplyArgs "
-       "a) {\n";
+       ") __attribute__((amdgpu_waves_per_eu(2))) void " + kernel_name(k, rows, copy_mask) +
+       "(const storb_rs::ApplyArgs a) {\n";
   if (lds >= 4) {
     // Static LDS reserving 160 KiB / cap per workgroup (occupancy cap).
     s += "  __shared__ unsigned occ_pad[" + std::to_string(lds / 4) + "];\n";
@@ -384,7 +393,8 @@ static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *c
   std::memcpy(&key[0], hdr, sizeof(hdr));
   std::memcpy(&key[32], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
-  auto e = J.get(key, [&] { return source(k, r, coef, copy_mask, group, sh, lds); });
+  auto e = J.get(key, kernel_name(k, r, copy_mask),
+                 [&] { return source(k, r, coef, copy_mask, group, sh, lds); });
   if (e && wait) J.wait_for(*e);
   return e;
 }

@@ -25,6 +25,9 @@ trace config2
 trace config5 --config 5
 trace config5_erase8 --config 5 --erase 8
 trace config6_erase16 --config 6 --erase 16
+trace config3 --config 3
+trace config4 --config 4
+trace config7 --config 7
 timeout -k 10 400 python3 bench.py > "$OUT/bench_default.log" 2>&1
 echo "default bench done"
 echo done
