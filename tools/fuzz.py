@@ -26,7 +26,7 @@ from oracle import coracle  # noqa: E402  (the checker)
 from storb_amd import _lib  # noqa: E402
 
 GEOS = [(1, 2), (2, 3), (4, 6), (8, 12), (16, 24), (32, 48), (3, 5), (5, 9), (6, 7), (10, 20),
-        (1, 1), (7, 7), (20, 30), (40, 60)]
+        (1, 1), (7, 7), (20, 30), (40, 60), (64, 96)]
 
 
 def rnd(rng, n):
