@@ -27,6 +27,9 @@ struct PermTab;  // gf256.hpp (host side only)
 // output once instead of XOR-accumulating it over column tiles.
 constexpr int kSlotK = 32;
 constexpr int kSlotR = 16;
+// Output slots of one launch: the table kernel fills kSlotR of them, the
+// row-split bit-sliced kernels (rs_bitslice_core.h) up to 32.
+constexpr int kMaxOut = 32;
 #ifndef STORB_RS_MAX_IN
 #define STORB_RS_MAX_IN 64  // (tools: -DSTORB_RS_MAX_IN=32 for a kernel-argument-size A/B)
 #endif
@@ -39,8 +42,8 @@ constexpr uint32_t kCopyMaxK = 16;
 struct ApplyArgs {
   const uint8_t *in[kMaxIn];
   uint64_t in_stride[kMaxIn];
-  uint8_t *out[kSlotR];
-  uint64_t out_stride[kSlotR];
+  uint8_t *out[kMaxOut];
+  uint64_t out_stride[kMaxOut];
   const PermTab *ptab;  // nibble tables [col][tab_rows], rows >= r zeroed
   const uint8_t *btab;  // 256-byte product tables, same order (LDS variant)
   uint32_t k, r;
@@ -103,6 +106,20 @@ constexpr int bs_group(int K, int R) {
                                          ? 8
                                          : (K % 4 == 0 ? 4 : (K % 2 == 0 ? 2 : 1)))));
 }
+
+// Row-split kernels (rs_bitslice_core.h bs_split_body; matrices of 17-32
+// rows, i.e. Storb's k = 64 encode and decodes losing more than 16 shares):
+// 128 lanes (one row half per wave), one input per wave per load group, 4
+// workgroups per CU (2 waves per SIMD at ~197 VGPRs). tools/k64split.hip,
+// k = 64 encode of 8 x 128 MiB chunks: 494.6 us as two 16-row launches ->
+// 348.6 us; 3 per CU 556 us (6 waves per CU), uncapped 391, 2 inputs per
+// wave per group 376.
+constexpr int kSplitGroup = 2;
+constexpr int kSplitCap = 4;
+constexpr int kSplitThreads = 128;           // two waves, one row half each
+constexpr unsigned kSplitColsPerTile = 128;  // 64 lanes x 2 16-B columns
+// Static LDS of one workgroup: [group parity][owner wave][G/2 inputs][2 halves][64 lanes] x 16 B.
+constexpr unsigned split_lds_bytes(int G) { return 2u * 2u * static_cast<unsigned>(G / 2) * 2u * 64u * 16u; }
 
 }  // namespace bs
 

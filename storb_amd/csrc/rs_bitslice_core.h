@@ -243,6 +243,137 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
 // rotates the tile order of stripe s by s * (tiles / 8 + 1), so the
 // workgroups of neighbouring stripes that run at the same moment stream
 // from different offsets of their shares (tools/wide_probe.hip).
+// ------------------------------------------------------------ row-split form
+// Matrices of more than 16 rows (Storb's k = 64 geometry: 32 parity rows,
+// and decodes losing more than 16 shares of it). One lane cannot hold 32 x 8
+// accumulator planes, so round 1 ran two 16-row launches that each read and
+// bit-sliced every input: 160 bytes moved per 96 algorithmic and the
+// transposes done twice. Here the two waves of a 128-lane workgroup cover
+// the SAME 2 KiB of every share and split the rows: wave w folds rows
+// [w ? RA : 0, w ? R : RA). Each input is loaded and transposed once, by the
+// wave that owns it (half of every load group), which publishes its 8
+// bit-planes through LDS; both waves fold every input into their own rows.
+// One barrier per load group, LDS double-buffered by group parity.
+
+// Rows [R0, R1) of matrix M, as a matrix type of their own.
+template <class M, int R0, int R1>
+struct RowSlice {
+  static constexpr int K = M::K, R = R1 - R0;
+  static constexpr unsigned long long copy_mask = M::copy_mask;
+  struct Net {
+    unsigned char row[R][K][8];
+  };
+  static constexpr Net make() {
+    Net n{};
+    for (int p = 0; p < R; p++)
+      for (int j = 0; j < K; j++)
+        for (int b = 0; b < 8; b++) n.row[p][j][b] = M::net.row[R0 + p][j][b];
+    return n;
+  }
+  static constexpr Net net = make();
+};
+
+// Launch shape: kSplitThreads lanes, kSplitGroup, kSplitCap (rs_args.h).
+// LDS of one workgroup: [group parity][owner wave][G/2 inputs][2 halves][64 lanes].
+template <int G>
+struct SplitLds {
+  v4 v[2 * 2 * (G / 2) * 2 * 64];
+};
+static_assert(sizeof(SplitLds<2>) == split_lds_bytes(2) && sizeof(SplitLds<4>) == split_lds_bytes(4),
+              "rs_args.h split_lds_bytes");
+
+// Waits for this wave's LDS writes, then the workgroup barrier. A compiler
+// memory barrier too: no LDS access moves across it. (Not __syncthreads():
+// its workgroup-scope fences also wait for the next group's global loads.)
+__device__ __forceinline__ void split_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <class M, int G, int W>
+__device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t stripe, uint32_t v0,
+                                              uint32_t cols, uint32_t lane, v4 *lds) {
+  constexpr int K = M::K, R = M::R, H = G / 2, RA = (R + 1) / 2;
+  static_assert(G % 2 == 0 && K % G == 0, "split groups: an even count dividing k");
+  using MW = RowSlice<M, W ? RA : 0, W ? R : RA>;
+  constexpr int RW = MW::R;
+  uint32_t acc[RW][8];
+#pragma unroll
+  for (int p = 0; p < RW; p++)
+#pragma unroll
+    for (int b = 0; b < 8; b++) acc[p][b] = 0;
+
+  v4 buf[2][H][2];
+  uint32_t ca = v0 < cols ? v0 : cols - 1, cb = v0 + 64 < cols ? v0 + 64 : cols - 1;
+  load_group<H>(a, W * H, stripe, ca, cb, buf[0]);
+  static_for<K / G>([&](auto GI) {
+    constexpr int gi = decltype(GI)::value;
+    if constexpr (K > 32) asm volatile("" : "+v"(ca), "+v"(cb));
+    if constexpr (gi + 1 < K / G)
+      load_group<H>(a, (gi + 1) * G + W * H, stripe, ca, cb, buf[(gi + 1) & 1]);
+    // Own inputs: fused-assembly copy, bit-slice, publish, fold.
+    static_for<H>([&](auto HH) {
+      constexpr int h = decltype(HH)::value;
+      constexpr int j = gi * G + W * H + h;
+      const v4 &A = buf[gi & 1][h][0], &Bv = buf[gi & 1][h][1];
+      if constexpr (((M::copy_mask >> j) & 1ull) != 0) {
+        v4 *c = reinterpret_cast<v4 *>(a.copy[j] + static_cast<uint64_t>(stripe) * a.copy_stride[j]);
+        if (v0 < cols) st_nt(c + v0, A);
+        if (v0 + 64 < cols) st_nt(c + v0 + 64, Bv);
+      }
+      uint32_t x[8] = {A[0], A[1], A[2], A[3], Bv[0], Bv[1], Bv[2], Bv[3]};
+      asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                   "+v"(x[6]), "+v"(x[7]));
+      transpose8(x);
+      v4 *slot = lds + ((((gi & 1) * 2 + W) * H + h) * 2) * 64 + lane;
+      slot[0] = v4{x[0], x[1], x[2], x[3]};
+      slot[64] = v4{x[4], x[5], x[6], x[7]};
+      fold_planes<MW, j>(acc, x);
+      fence_acc(acc);
+    });
+    split_barrier();
+    // The other wave's inputs of this group, from LDS.
+    static_for<H>([&](auto HH) {
+      constexpr int h = decltype(HH)::value;
+      constexpr int j = gi * G + (1 - W) * H + h;
+      const v4 *slot = lds + ((((gi & 1) * 2 + (1 - W)) * H + h) * 2) * 64 + lane;
+      const v4 P = slot[0], Q = slot[64];
+      uint32_t x[8] = {P[0], P[1], P[2], P[3], Q[0], Q[1], Q[2], Q[3]};
+      fold_planes<MW, j>(acc, x);
+      fence_acc(acc);
+    });
+  });
+
+  constexpr int r0 = W ? RA : 0;
+#pragma unroll
+  for (int p = 0; p < RW; p++) {
+    transpose8(acc[p]);
+    v4 *q = reinterpret_cast<v4 *>(a.out[r0 + p] + static_cast<uint64_t>(stripe) * a.out_stride[r0 + p]);
+    const v4 A = {acc[p][0], acc[p][1], acc[p][2], acc[p][3]};
+    const v4 Bv = {acc[p][4], acc[p][5], acc[p][6], acc[p][7]};
+    if (v0 < cols) st_nt(q + v0, A);
+    if (v0 + 64 < cols) st_nt(q + v0 + 64, Bv);
+  }
+}
+
+// Grid: nstripes x tiles of kSplitColsPerTile columns, kSplitThreads lanes.
+template <class M, int G, int SWZ = 0>
+__device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
+  __shared__ SplitLds<G> lds;
+  constexpr uint32_t CPT = kSplitColsPerTile;
+  const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
+  const uint32_t tps = (cols + CPT - 1) / CPT;
+  const uint32_t stripe = blockIdx.x / tps;
+  uint32_t tile = blockIdx.x - stripe * tps;
+  if constexpr (SWZ == 1) tile = (tile + stripe * (tps / 8 + 1)) % tps;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t v0 = tile * CPT + lane;
+  // wave-uniform (an SGPR), so the two row halves are scalar branches
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
+    bs_split_wave<M, G, 0>(a, stripe, v0, cols, lane, lds.v);
+  else
+    bs_split_wave<M, G, 1>(a, stripe, v0, cols, lane, lds.v);
+}
+
 template <class M, int G, int T = kBsThreads, int SWZ = 0>
 __device__ __forceinline__ void bs_kernel_body(const ApplyArgs &a) {
   constexpr uint32_t CPT = bs_cols_per_tile(T);

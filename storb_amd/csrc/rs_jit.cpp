@@ -287,8 +287,8 @@ Jit &jit() {
 }
 
 // Launch shape (rs_args.h bs_shape, shared with the ahead-of-time
-// encoders); the resident-workgroup cap is baked into the kernel as static
-// LDS (rs_kernels.hpp cap_lds).
+// encoders); the resident-workgroup cap is an LDS reservation
+// (rs_kernels.hpp cap_lds, see dynamic_lds()).
 // STORB_RS_JIT_SHAPE="threads,swz,cap" overrides it for every compiled
 // kernel (launch-shape A/B on the real decode path without a rebuild).
 bs::BsShape shape(uint32_t k, uint32_t r) {
@@ -303,6 +303,31 @@ bs::BsShape shape(uint32_t k, uint32_t r) {
   return s;
 }
 
+bool split_rows(uint32_t k, uint32_t rows);
+
+// The row-split kernels' shape (rs_args.h kSplitCap; the cap alone follows
+// STORB_RS_WG_PER_CU), or shape().
+bs::BsShape split_or_shape(uint32_t k, uint32_t r) {
+  if (!split_rows(k, r)) return shape(k, r);
+  return bs::BsShape{bs::kSplitThreads, 0, wg_cap(bs::kSplitCap)};
+}
+
+// The cap's LDS reservation is requested at launch (dynamic LDS) when it is
+// at most 64 KiB (caps >= 3; above that a kernel must opt in) and baked into
+// the source as a static array otherwise. Static LDS that limits occupancy
+// to 2 waves per SIMD told the register allocator it could use all 256
+// VGPRs, and it did: the k = 64 row-split encode took 256 VGPRs with 7
+// spilled (0.535 ms in bench --config 7) against 197 and none with the same
+// reservation made at launch (0.349 ms in tools/k64split.hip); likewise the
+// 16-row blocks 229 vs 196. STORB_RS_JIT_STATIC_LDS=1 keeps it static (A/B).
+size_t dynamic_lds(size_t lds) {
+  static const bool force_static = [] {
+    const char *e = std::getenv("STORB_RS_JIT_STATIC_LDS");
+    return e && e[0] == '1';
+  }();
+  return !force_static && lds <= (64u << 10) ? lds : 0;
+}
+
 // Kernel symbol, so profiles tell the compiled kernels apart (bench.py and
 // profiles/summarize.py match on the "storb_bs_jit_k<k>_r<rows>_" prefix).
 std::string kernel_name(uint32_t k, uint32_t rows, uint64_t copy_mask) {
@@ -310,10 +335,27 @@ std::string kernel_name(uint32_t k, uint32_t rows, uint64_t copy_mask) {
          (copy_mask ? "_asm" : "_ip");
 }
 
+// Matrices of 17-32 rows run as ONE row-split launch (rs_bitslice_core.h
+// bs_split_body: each input read and bit-sliced once, its planes shared by
+// the two row-half waves through LDS) instead of row blocks of <= kSlotR
+// that each re-read every input. Needs an even k (one input per wave per
+// load group). STORB_RS_JIT_SPLIT=0 restores the row blocks (A/B).
+bool split_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("STORB_RS_JIT_SPLIT");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+bool split_rows(uint32_t k, uint32_t rows) {
+  return split_on() && rows > static_cast<uint32_t>(kSlotR) && rows <= kMaxRows &&
+         k % bs::kSplitGroup == 0;
+}
+
 // The kernel source for a (rows x k) matrix: bit b' of row[p][j][b] is bit b
 // of coef[p][j] * 2^b' (the GF(2) matrix of multiplication by coef[p][j]).
 std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask,
-                   int group, const bs::BsShape &sh, size_t lds) {
+                   int group, const bs::BsShape &sh, size_t lds, bool split) {
   const GF256 &g = gf();
   std::string s;
   s.reserve(64 + static_cast<size_t>(rows) * k * 40);
@@ -343,13 +385,17 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
   s += "extern \"C\" __global__ __launch_bounds__(" + std::to_string(sh.threads) +
        ") __attribute__((amdgpu_waves_per_eu(2))) void " + kernel_name(k, rows, copy_mask) +
        "(const storb_rs::ApplyArgs a) {\n";
-  if (lds >= 4) {
+  if (lds >= 4 && dynamic_lds(lds) == 0) {
     // Static LDS reserving 160 KiB / cap per workgroup (occupancy cap).
     s += "  __shared__ unsigned occ_pad[" + std::to_string(lds / 4) + "];\n";
     s += "  asm volatile(\"\" :: \"s\"(occ_pad));  // keeps the unused array allocated\n";
   }
-  s += "  storb_rs::bs::bs_kernel_body<JitMat, " + std::to_string(group) + ", " +
-       std::to_string(sh.threads) + ", " + std::to_string(sh.swz) + ">(a);\n}\n";
+  if (split)
+    s += "  storb_rs::bs::bs_split_body<JitMat, " + std::to_string(group) + ", " +
+         std::to_string(sh.swz) + ">(a);\n}\n";
+  else
+    s += "  storb_rs::bs::bs_kernel_body<JitMat, " + std::to_string(group) + ", " +
+         std::to_string(sh.threads) + ", " + std::to_string(sh.swz) + ">(a);\n}\n";
   return s;
 }
 
@@ -383,27 +429,32 @@ bool wanted(uint32_t k, uint32_t rows, uint64_t bytes) {
 // or created and queued. wait: block until its compile has finished.
 static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *coef,
                                         uint64_t copy_mask, bool wait) {
-  const int group = bs::bs_group(static_cast<int>(k), static_cast<int>(r));
-  const bs::BsShape sh = shape(k, r);
-  const size_t lds = cap_lds(sh.cap, 0);
+  const bool split = split_rows(k, r);
+  const int group = split ? bs::kSplitGroup : bs::bs_group(static_cast<int>(k), static_cast<int>(r));
+  const bs::BsShape sh = split_or_shape(k, r);
+  const size_t lds = cap_lds(sh.cap, split ? bs::split_lds_bytes(bs::kSplitGroup) : 0);
   std::string key(32 + static_cast<size_t>(r) * k, '\0');
   const uint64_t hdr[4] = {(static_cast<uint64_t>(k) << 32) | r, copy_mask,
                            (static_cast<uint64_t>(group) << 32) | lds,
-                           (static_cast<uint64_t>(sh.threads) << 32) | static_cast<uint32_t>(sh.swz)};
+                           (static_cast<uint64_t>(sh.threads) << 32) | static_cast<uint32_t>(sh.swz) |
+                               (split ? 1ull << 16 : 0)};
   std::memcpy(&key[0], hdr, sizeof(hdr));
   std::memcpy(&key[32], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
   auto e = J.get(key, kernel_name(k, r, copy_mask),
-                 [&] { return source(k, r, coef, copy_mask, group, sh, lds); });
+                 [&] { return source(k, r, coef, copy_mask, group, sh, lds, split); });
   if (e && wait) J.wait_for(*e);
   return e;
 }
 
 // Row blocks of at most kSlotR rows (the accumulators of one launch), as
 // even as possible: 20 rows -> 10 + 10. Block b covers rows [r0(b), r0(b+1)).
-static uint32_t row_blocks(uint32_t rows) { return (rows + kSlotR - 1) / kSlotR; }
-static uint32_t row_start(uint32_t rows, uint32_t b) {
-  const uint32_t nb = row_blocks(rows);
+// A row-split matrix is one block of all its rows.
+static uint32_t row_blocks(uint32_t k, uint32_t rows) {
+  return split_rows(k, rows) ? 1 : (rows + kSlotR - 1) / kSlotR;
+}
+static uint32_t row_start(uint32_t k, uint32_t rows, uint32_t b) {
+  const uint32_t nb = row_blocks(k, rows);
   return static_cast<uint32_t>(static_cast<uint64_t>(rows) * b / nb);
 }
 
@@ -430,11 +481,11 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
   // split between the compiled and the table kernels); the first block
   // also does the fused-assembly copies.
   Jit &J = jit();
-  const uint32_t nb = row_blocks(a.r);
+  const uint32_t nb = row_blocks(a.k, a.r);
   std::vector<std::shared_ptr<Entry>> es(nb);
   bool ready = true;
   for (uint32_t b = 0; b < nb; b++) {
-    const uint32_t r0 = row_start(a.r, b), rr = row_start(a.r, b + 1) - r0;
+    const uint32_t r0 = row_start(a.k, a.r, b), rr = row_start(a.k, a.r, b + 1) - r0;
     es[b] = entry_for(a.k, rr, coef + static_cast<size_t>(r0) * a.k, b == 0 ? copy_mask : 0,
                       false);
     ready = ready && es[b] && es[b]->state == Entry::Ready;
@@ -456,9 +507,10 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
   // profiles/r2_k64/.)
   hipError_t r = hipSuccess;
   for (uint32_t b = 0; b < nb && r == hipSuccess; b++) {
-    const uint32_t r0 = row_start(a.r, b), rr = row_start(a.r, b + 1) - r0;
-    const bs::BsShape sh = shape(a.k, rr);
-    const uint64_t cpt = bs::bs_cols_per_tile(sh.threads);
+    const uint32_t r0 = row_start(a.k, a.r, b), rr = row_start(a.k, a.r, b + 1) - r0;
+    const bs::BsShape sh = split_or_shape(a.k, rr);
+    const uint64_t cpt =
+        split_rows(a.k, rr) ? bs::kSplitColsPerTile : bs::bs_cols_per_tile(sh.threads);
     const uint64_t blocks = ((cols + cpt - 1) / cpt) * a.nstripes;
     if (blocks == 0 || blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     ApplyArgs arg = a;
@@ -472,8 +524,10 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
       arg.out_stride[i] = out_stride[r0 + i];
     }
     void *params[] = {&arg};
+    const size_t lds = cap_lds(sh.cap, split_rows(a.k, rr) ? bs::split_lds_bytes(bs::kSplitGroup) : 0);
     r = hipModuleLaunchKernel(fs[b], static_cast<unsigned>(blocks), 1, 1,
-                              static_cast<unsigned>(sh.threads), 1, 1, 0, s, params, nullptr);
+                              static_cast<unsigned>(sh.threads), 1, 1,
+                              static_cast<unsigned>(dynamic_lds(lds)), s, params, nullptr);
     if (r == hipSuccess) J.launches++;
   }
   if (r != hipSuccess) return r;
@@ -484,8 +538,8 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
 int prepare(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask, bool wait) {
   if (!enabled() || !valu_bound(k, rows)) return 0;
   int res = 1;
-  for (uint32_t b = 0; b < row_blocks(rows); b++) {
-    const uint32_t r0 = row_start(rows, b), rr = row_start(rows, b + 1) - r0;
+  for (uint32_t b = 0; b < row_blocks(k, rows); b++) {
+    const uint32_t r0 = row_start(k, rows, b), rr = row_start(k, rows, b + 1) - r0;
     auto e = entry_for(k, rr, coef + static_cast<size_t>(r0) * k, b == 0 ? copy_mask : 0, wait);
     if (!e) return 0;
     if (e->state == Entry::Failed) return -1;

@@ -37,6 +37,15 @@ def launches():
     return _lib.jit_stats()["launches"]
 
 
+def jit_launches(k, rows):
+    """Launches of one compiled matrix (rs_jit.cpp): 17-32 rows at even k are
+    ONE row-split launch (rs_bitslice_core.h bs_split_body); otherwise row
+    blocks of <= 16 rows."""
+    if 16 < rows <= 32 and k % 2 == 0:
+        return 1
+    return -(-rows // 16)
+
+
 CASES = [
     # k, n, B, stripes, erased data shares (+ parity not offered); the policy
     # compiles k >= 12 from 2 lost rows, k = 8..11 from 6. Launch shapes
@@ -182,11 +191,17 @@ def test_jit_not_used_where_table_kernel_is_hbm_bound(ctx):
 def test_jit_k64_encode_and_decode(ctx):
     """Storb's widest geometry: objects from ~160 GiB are chunked at 128-256
     MiB and sized k = 64, m = 96 (piece.rs:292-317). Encode (32 parity rows)
-    and a 20-lost decode (20 rows) each run as two compiled launches of <= 16
-    rows that see all 64 inputs; an odd k = 40 decode too. Oracle-exact; the
-    compiles (several seconds each at k = 64) are waited for first."""
+    and a 20-lost decode (20 rows) each run as ONE row-split launch (two waves
+    per workgroup, 16 / 10 rows each, every input read once); a ragged share
+    size (last tile partly past the share end), a 17-row decode (rows split
+    9 + 8), k = 40 (20 parity rows split, 3-lost decode on one wave-size
+    kernel) and odd k = 41 (21 parity rows: two row blocks, no split) too.
+    Oracle-exact; the compiles (several seconds each at k = 64) are waited
+    for first."""
     for k, n, B, ns, erased in [(64, 96, 16 << 10, 4, list(range(20))),
-                                (40, 60, 32 << 10, 4, [0, 3, 33])]:
+                                (64, 96, (16 << 10) + 48, 4, list(range(3, 37, 2))),
+                                (40, 60, 32 << 10, 4, [0, 3, 33]),
+                                (41, 62, 16 << 10, 6, list(range(17)))]:
         data_h, par_h = oracle_batch(k, n, B, ns, 64 + k)
         data = torch.from_numpy(data_h).to(DEV)
         par = torch.zeros(ns * (n - k) * B, dtype=torch.uint8, device=DEV)
@@ -200,8 +215,7 @@ def test_jit_k64_encode_and_decode(ctx):
         before = launches()
         ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
         torch.cuda.synchronize()
-        blocks = -(-(n - k) // 16)
-        assert launches() == before + blocks, "compiled encode did not run"
+        assert launches() == before + jit_launches(k, n - k), "compiled encode did not run"
         assert np.array_equal(par.cpu().numpy(), par_h), (k, "compiled encode")
         view = data.view(ns, k, B)
         for e in erased:
@@ -209,7 +223,7 @@ def test_jit_k64_encode_and_decode(ctx):
         before = launches()
         ctx.decode_batch_dev(k, n, B, ns, surv, data.data_ptr(), par.data_ptr(), data.data_ptr())
         torch.cuda.synchronize()
-        assert launches() == before + -(-len(erased) // 16), "compiled decode did not run"
+        assert launches() == before + jit_launches(k, len(erased)), "compiled decode did not run"
         assert np.array_equal(data.cpu().numpy(), data_h), (k, "compiled decode")
 
 
@@ -218,8 +232,9 @@ def test_jit_k64_encode_and_decode(ctx):
 def test_jit_k64_decode_into_separate_buffer(ctx):
     """k = 64 decode into a fresh chunk buffer (decode_chunk semantics,
     piece.rs:363-387): the first row block's kernel also stores every
-    surviving data share to its slot (fused assembly, a 64-bit copy mask);
-    20 lost rows = two compiled launches. Oracle-exact, sources untouched."""
+    surviving data share to its slot (fused assembly, a 64-bit copy mask; in
+    the row-split kernel the wave that loads a share stores it); 20 lost rows
+    = one row-split launch. Oracle-exact, sources untouched."""
     k, n, B, ns = 64, 96, 16 << 10, 4
     erased = [0, 5, 9, 13, 17, 21, 25, 29, 33, 37, 41, 45, 49, 53, 57, 61, 62, 63, 1, 2]
     data_h, par_h = oracle_batch(k, n, B, ns, 6464)
@@ -234,7 +249,7 @@ def test_jit_k64_decode_into_separate_buffer(ctx):
     before = launches()
     ctx.decode_batch_dev(k, n, B, ns, surv, data.data_ptr(), par.data_ptr(), out.data_ptr())
     torch.cuda.synchronize()
-    assert launches() == before + 2
+    assert launches() == before + jit_launches(k, len(erased))
     assert np.array_equal(out.cpu().numpy(), data_h)
     for e in erased:
         assert bool((view[:, e] == 0xA5).all())

@@ -18,6 +18,8 @@ for ((r = 0; r < REPS; r++)); do
       c5) args="--config 5" ;;
       c5e*) args="--config 5 --erase ${c#c5e}" ;;
       c6e*) args="--config 6 --erase ${c#c6e}" ;;
+      c7) args="--config 7" ;;
+      c7e*) args="--config 7 --erase ${c#c7e}" ;;
     esac
     for sp in $SPECS; do
       envs=()
