@@ -427,9 +427,13 @@ def leg_rows(w, leg):
     return w.n - w.k if leg == "encode" else sum(1 for x in w.erased if x < w.k)
 
 
-def jit_blocks(rows):
-    """Compiled launches of a rows-row matrix (rs_jit.cpp: row blocks of <= 16,
-    balanced) and the first block's rows."""
+def jit_blocks(k, rows):
+    """Compiled launches of a rows-row matrix and the first launch's rows
+    (rs_jit.cpp): 17-32 rows at even k are one row-split launch
+    (STORB_RS_JIT_SPLIT=0: row blocks instead), otherwise row blocks of <= 16,
+    balanced."""
+    if 16 < rows <= 32 and k % 2 == 0 and os.environ.get("STORB_RS_JIT_SPLIT", "1")[:1] != "0":
+        return 1, rows
     nb = -(-rows // 16)
     return nb, rows // nb
 
@@ -438,7 +442,7 @@ def leg_kernel_match(a, w, leg):
     """Substring of the rocprofv3 kernel name each leg launches (compiled
     kernels are named storb_bs_jit_k<k>_r<rows>_{ip,asm}, rs_jit.cpp)."""
     if leg in w.jit_legs:
-        return f"storb_bs_jit_k{w.k}_r{jit_blocks(leg_rows(w, leg))[1]}_"
+        return f"storb_bs_jit_k{w.k}_r{jit_blocks(w.k, leg_rows(w, leg))[1]}_"
     if leg == "encode":
         if a.kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48)):
             return f"rs_encode_bitslice<{w.k}, {w.n}>"
@@ -516,7 +520,7 @@ def pmc_traffic(a, w):
 
 
 def jit_name(w, leg):
-    nb, r0 = jit_blocks(leg_rows(w, leg))
+    nb, r0 = jit_blocks(w.k, leg_rows(w, leg))
     return (f"storb_bs_jit_k{w.k}_r{r0}_* (hipRTC)"
             + (f" x {nb} row blocks" if nb > 1 else ""))
 
@@ -827,7 +831,7 @@ def main():
                               "separate untimed pass with an event after every leg"),
             "alg_bytes_per_launch": alg,
             "kernel_match": {leg: leg_kernel_match(a, w, leg) for leg in w.legs},
-            "launches_per_leg": {leg: jit_blocks(leg_rows(w, leg))[0] if leg in w.jit_legs
+            "launches_per_leg": {leg: jit_blocks(w.k, leg_rows(w, leg))[0] if leg in w.jit_legs
                                  else 1 for leg in w.legs},
             "copy_ceiling_gbs": None,
             "jit": {"launches_in_run": jit1["launches"] - jit0["launches"],
@@ -837,9 +841,9 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.minimal:
-        if not a.no_traffic and a.config == 7:
+        if not a.no_traffic and max(out["roofline"]["launches_per_leg"].values()) > 1:
             out["roofline"]["traffic_source"] = (
-                "not measured: config 7's legs are several compiled launches each (row blocks)")
+                "not measured: a leg is several compiled launches (row blocks)")
         elif not a.no_traffic:
             pmc = pmc_traffic(a, w)
             out["roofline"].update(pmc)

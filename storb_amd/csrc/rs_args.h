@@ -107,15 +107,22 @@ constexpr int bs_group(int K, int R) {
                                          : (K % 4 == 0 ? 4 : (K % 2 == 0 ? 2 : 1)))));
 }
 
-// Row-split kernels (rs_bitslice_core.h bs_split_body; matrices of 17-32
-// rows, i.e. Storb's k = 64 encode and decodes losing more than 16 shares):
-// 128 lanes (one row half per wave), one input per wave per load group, 4
-// workgroups per CU (2 waves per SIMD at ~197 VGPRs). tools/k64split.hip,
-// k = 64 encode of 8 x 128 MiB chunks: 494.6 us as two 16-row launches ->
-// 348.6 us; 3 per CU 556 us (6 waves per CU), uncapped 391, 2 inputs per
-// wave per group 376.
+// Row-split kernels (rs_bitslice_core.h bs_split_body): 128 lanes (one row
+// half per wave), one input per wave per load group. Used (bs_split)
+//  * for 17-32 rows -- Storb's k = 64 encode and decodes losing more than 16
+//    shares -- which one wave cannot hold: 4 workgroups per CU (2 waves per
+//    SIMD at ~197 VGPRs). tools/k64split.hip, k = 64 encode of 8 x 128 MiB
+//    chunks: 494.6 us as two 16-row launches -> 348.6 us; 3 per CU 556 us
+//    (6 waves per CU), uncapped 391, 2 inputs per wave per group 376
+//    (profiles/r2_k64/k64split.txt);
+//  * not for 16 rows or fewer: RS(32,16) with 8 rows per wave (127 VGPRs, 6
+//    per CU) measured 274.8 -> 267.7 us in isolation
+//    (profiles/r2_k64/k64split2.txt) but nothing in the product (bench
+//    --config 6 --erase 16: decode 0.2709 ms one wave per tile, 0.2720
+//    split, profiles/r2_k64/split_k32_ab.txt); RS(16,8) within noise.
 constexpr int kSplitGroup = 2;
-constexpr int kSplitCap = 4;
+constexpr bool bs_split(int K, int R) { return K % kSplitGroup == 0 && R > 16 && R <= 32; }
+constexpr int bs_split_cap(int R) { return R > 16 ? 4 : 6; }
 constexpr int kSplitThreads = 128;           // two waves, one row half each
 constexpr unsigned kSplitColsPerTile = 128;  // 64 lanes x 2 16-B columns
 // Static LDS of one workgroup: [group parity][owner wave][G/2 inputs][2 halves][64 lanes] x 16 B.

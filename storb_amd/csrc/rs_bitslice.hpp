@@ -97,30 +97,39 @@ struct EncMat {
   static constexpr Bits<K_, N_> net = make_bits<K_, N_>();
 };
 
-// Launch shape per geometry (rs_args.h bs_shape).
+// Launch shape per geometry (rs_args.h bs_shape, or the row-split form
+// where bs_split says so -- more than 16 parity rows; none of the two AOT
+// geometries today).
 template <int K, int N>
 struct BsTune {
+  static constexpr bool SPLIT = bs_split(K, N - K);
   static constexpr BsShape S = bs_shape(K, N - K);
-  static constexpr int T = S.threads, SWZ = S.swz, OCC = S.cap;
-  static constexpr int G = bs_group(K, N - K);
+  static constexpr int T = SPLIT ? kSplitThreads : S.threads, SWZ = SPLIT ? 0 : S.swz;
+  static constexpr int OCC = SPLIT ? bs_split_cap(N - K) : S.cap;
+  static constexpr int G = SPLIT ? kSplitGroup : bs_group(K, N - K);
+  static constexpr uint64_t CPT = SPLIT ? kSplitColsPerTile : bs_cols_per_tile(T);
+  static constexpr size_t LDS = SPLIT ? split_lds_bytes(kSplitGroup) : 0;
 };
 
 template <int K, int N>
 __global__ __launch_bounds__((BsTune<K, N>::T)) __attribute__((amdgpu_waves_per_eu(2))) void
 rs_encode_bitslice(const ApplyArgs a) {
   using C = BsTune<K, N>;
-  bs_kernel_body<EncMat<K, N>, C::G, C::T, C::SWZ>(a);
+  if constexpr (C::SPLIT)
+    bs_split_body<EncMat<K, N>, C::G, C::SWZ>(a);
+  else
+    bs_kernel_body<EncMat<K, N>, C::G, C::T, C::SWZ>(a);
 }
 
 template <int K, int N>
 hipError_t launch_bitslice(const ApplyArgs &a, hipStream_t s) {
   using C = BsTune<K, N>;
-  constexpr uint64_t cpt = bs_cols_per_tile(C::T);
+  constexpr uint64_t cpt = C::CPT;
   const uint64_t cols = a.block >> 4;
   const uint64_t blocks = ((cols + cpt - 1) / cpt) * a.nstripes;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  return launch_lds<rs_encode_bitslice<K, N>>(blocks, C::T, cap_lds(wg_cap(C::OCC), 0), s, a);
+  return launch_lds<rs_encode_bitslice<K, N>>(blocks, C::T, cap_lds(wg_cap(C::OCC), C::LDS), s, a);
 }
 
 }  // namespace bs

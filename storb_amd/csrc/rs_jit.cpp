@@ -305,11 +305,11 @@ bs::BsShape shape(uint32_t k, uint32_t r) {
 
 bool split_rows(uint32_t k, uint32_t rows);
 
-// The row-split kernels' shape (rs_args.h kSplitCap; the cap alone follows
+// The row-split kernels' shape (rs_args.h bs_split_cap; the cap alone follows
 // STORB_RS_WG_PER_CU), or shape().
 bs::BsShape split_or_shape(uint32_t k, uint32_t r) {
   if (!split_rows(k, r)) return shape(k, r);
-  return bs::BsShape{bs::kSplitThreads, 0, wg_cap(bs::kSplitCap)};
+  return bs::BsShape{bs::kSplitThreads, 0, wg_cap(bs::bs_split_cap(static_cast<int>(r)))};
 }
 
 // The cap's LDS reservation is requested at launch (dynamic LDS) when it is
@@ -338,8 +338,9 @@ std::string kernel_name(uint32_t k, uint32_t rows, uint64_t copy_mask) {
 // Matrices of 17-32 rows run as ONE row-split launch (rs_bitslice_core.h
 // bs_split_body: each input read and bit-sliced once, its planes shared by
 // the two row-half waves through LDS) instead of row blocks of <= kSlotR
-// that each re-read every input. Needs an even k (one input per wave per
-// load group). STORB_RS_JIT_SPLIT=0 restores the row blocks (A/B).
+// that each re-read every input (rs_args.h bs_split). Needs an even k (one
+// input per wave per load group). STORB_RS_JIT_SPLIT=0 restores the row
+// blocks (A/B).
 bool split_on() {
   static const bool on = [] {
     const char *e = std::getenv("STORB_RS_JIT_SPLIT");
@@ -348,8 +349,7 @@ bool split_on() {
   return on;
 }
 bool split_rows(uint32_t k, uint32_t rows) {
-  return split_on() && rows > static_cast<uint32_t>(kSlotR) && rows <= kMaxRows &&
-         k % bs::kSplitGroup == 0;
+  return split_on() && rows <= kMaxRows && bs::bs_split(static_cast<int>(k), static_cast<int>(rows));
 }
 
 // The kernel source for a (rows x k) matrix: bit b' of row[p][j][b] is bit b

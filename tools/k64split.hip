@@ -1,11 +1,12 @@
-// k64split.hip -- Storb's k = 64 encode (32 parity rows): the product's two
-// 16-row launches (rs_jit.cpp row blocks, each reading and bit-slicing all 64
-// inputs) against ONE row-split launch (rs_bitslice_core.h bs_split_body: the
-// two waves of a 128-lane workgroup share each input's bit-planes through
-// LDS and fold 16 rows each), over load-group size G and the
-// resident-workgroup cap. Also RS(32,16)-like 20- and 24-row decodes at k = 64
-// (split vs two blocks). Every variant is compared bit-exactly with the
-// two-launch form.
+// k64split.hip -- the row-split bit-sliced kernel (rs_bitslice_core.h
+// bs_split_body: the two waves of a 128-lane workgroup share each input's
+// bit-planes through LDS and fold half the rows each) over load-group size G
+// and the resident-workgroup cap, against:
+//   RS(64,32) encode: the two 16-row launches the product ran before (each
+//     reading and bit-slicing all 64 inputs);
+//   RS(32,16) / RS(16,8) encode: the product's one-wave-per-tile kernel (is
+//     splitting 16 or 8 rows over two waves worth its extra table work?).
+// Every variant is compared bit-exactly with the first of its geometry.
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../storb_amd/csrc \
 //        -fconstexpr-steps=100000000 k64split.hip -o _build/k64split
@@ -37,16 +38,10 @@ int storb_rs::table_threads_override() { return 0; }
     }                                                                          \
   } while (0)
 
-using Enc = EncMat<64, 96>;
-using Lo = RowSlice<Enc, 0, 16>;
-using Hi = RowSlice<Enc, 16, 32>;
-constexpr int G16 = bs_group(64, 16);
-constexpr int T = 128;
-
-template <class M>
+template <class M, int G, int T, int SWZ>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_single(
     const ApplyArgs a) {
-  bs_kernel_body<M, G16, T, 0>(a);
+  bs_kernel_body<M, G, T, SWZ>(a);
 }
 
 template <class M, int G>
@@ -56,12 +51,13 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(2
 }
 
 template <auto Kern, typename... Args>
-hipError_t launch(uint64_t blocks, int cap, size_t static_lds, hipStream_t s, Args... args) {
+hipError_t launch(uint64_t blocks, int threads, int cap, size_t static_lds, hipStream_t s,
+                  Args... args) {
   const size_t dyn = cap_lds(cap, static_lds);
   if (dyn > (64u << 10))
     CK(hipFuncSetAttribute(reinterpret_cast<const void *>(Kern),
                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(dyn)));
-  hipLaunchKernelGGL(Kern, dim3(blocks), dim3(T), dyn, s, args...);
+  hipLaunchKernelGGL(Kern, dim3(blocks), dim3(threads), dyn, s, args...);
   return hipGetLastError();
 }
 
@@ -81,10 +77,11 @@ struct V {
   std::vector<float> us;
 };
 
-int main(int argc, char **argv) {
-  const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
-  const uint64_t B = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (2u << 20);
-  const uint32_t ns = argc > 3 ? std::atoi(argv[3]) : 8, K = 64, R = 32;
+// Storb-sized batch of 1 GiB of data: (k, n) shares of B bytes, ns stripes.
+template <int K, int N>
+int run(int rounds, uint64_t B, uint32_t ns) {
+  constexpr int R = N - K;
+  using Enc = EncMat<K, N>;
   const uint64_t in_bytes = (uint64_t)ns * K * B, out_bytes = (uint64_t)ns * R * B;
   uint8_t *in, *out;
   CK(hipMalloc(&in, in_bytes));
@@ -92,39 +89,52 @@ int main(int argc, char **argv) {
   hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, in_bytes / 8, 64);
   ApplyArgs a{};
   a.k = K;
-  a.r = 32;
+  a.r = R;
   for (uint32_t j = 0; j < K; j++) {
     a.in[j] = in + j * B;
     a.in_stride[j] = K * B;
   }
-  for (int i = 0; i < 32; i++) {
+  for (int i = 0; i < R; i++) {
     a.out[i] = out + i * B;
     a.out_stride[i] = R * B;
   }
   a.block = B;
   a.nstripes = ns;
-  ApplyArgs alo = a, ahi = a;
-  alo.r = ahi.r = 16;
-  for (int i = 0; i < 16; i++) {
-    ahi.out[i] = a.out[16 + i];
-    ahi.out_stride[i] = a.out_stride[16 + i];
-  }
   const uint64_t cols = B / 16;
-  const uint64_t tiles1 = ((cols + bs_cols_per_tile(T) - 1) / bs_cols_per_tile(T)) * ns;
   const uint64_t tiles2 = ((cols + kSplitColsPerTile - 1) / kSplitColsPerTile) * ns;
   std::vector<V> vs;
-  for (int cap : {3, 4}) {
-    vs.push_back({"two launches cap=" + std::to_string(cap), [=](hipStream_t s) {
-                    CK(launch<k_single<Lo>>(tiles1, cap, 0, s, alo));
-                    CK(launch<k_single<Hi>>(tiles1, cap, 0, s, ahi));
+  if constexpr (R > 16) {
+    // the product before the row split: two 16-row launches
+    using Lo = RowSlice<Enc, 0, R / 2>;
+    using Hi = RowSlice<Enc, R / 2, R>;
+    constexpr BsShape S = bs_shape(K, R / 2);
+    constexpr int G = bs_group(K, R / 2);
+    ApplyArgs alo = a, ahi = a;
+    alo.r = ahi.r = R / 2;
+    for (int i = 0; i < R / 2; i++) {
+      ahi.out[i] = a.out[R / 2 + i];
+      ahi.out_stride[i] = a.out_stride[R / 2 + i];
+    }
+    const uint64_t tiles1 = ((cols + bs_cols_per_tile(S.threads) - 1) / bs_cols_per_tile(S.threads)) * ns;
+    vs.push_back({"two launches (old product)", [=](hipStream_t s) {
+                    CK((launch<k_single<Lo, G, S.threads, S.swz>>(tiles1, S.threads, S.cap, 0, s, alo)));
+                    CK((launch<k_single<Hi, G, S.threads, S.swz>>(tiles1, S.threads, S.cap, 0, s, ahi)));
+                  }, {}});
+  } else {
+    // the product: one launch, every row in one wave
+    constexpr BsShape S = bs_shape(K, R);
+    constexpr int G = bs_group(K, R);
+    const uint64_t tiles1 = ((cols + bs_cols_per_tile(S.threads) - 1) / bs_cols_per_tile(S.threads)) * ns;
+    vs.push_back({"one wave per tile (product)", [=](hipStream_t s) {
+                    CK((launch<k_single<Enc, G, S.threads, S.swz>>(tiles1, S.threads, S.cap, 0, s, a)));
                   }, {}});
   }
-  for (int cap : {2, 3, 4, 0}) {
+  for (int cap : {4, 6, 8, 0}) {
     vs.push_back({"split G=2 cap=" + std::to_string(cap), [=](hipStream_t s) {
-                    CK((launch<k_split<Enc, 2>>(tiles2, cap, sizeof(SplitLds<2>), s, a)));
+                    CK((launch<k_split<Enc, 2>>(tiles2, kSplitThreads, cap, sizeof(SplitLds<2>), s, a)));
                   }, {}});
     vs.push_back({"split G=4 cap=" + std::to_string(cap), [=](hipStream_t s) {
-                    CK((launch<k_split<Enc, 4>>(tiles2, cap, sizeof(SplitLds<4>), s, a)));
+                    CK((launch<k_split<Enc, 4>>(tiles2, kSplitThreads, cap, sizeof(SplitLds<4>), s, a)));
                   }, {}});
   }
   hipStream_t s;
@@ -155,13 +165,25 @@ int main(int argc, char **argv) {
       v.us.push_back(ms * 1000.f / 4);
     }
   const double bytes = (double)in_bytes + out_bytes;
-  std::printf("k=64 encode (32 rows), %u x %llu-B shares: %.3f GB algorithmic, bit-exact\n", ns,
-              (unsigned long long)B, bytes / 1e9);
+  std::printf("RS(%d,%d) encode (%d rows), %u x %llu-B shares: %.3f GB algorithmic, bit-exact\n",
+              K, R, R, ns, (unsigned long long)B, bytes / 1e9);
   for (auto &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
     std::printf("  %-26s %8.1f us  %7.1f GB/s  %.1f%% of 8 TB/s\n", v.name.c_str(), med,
                 bytes / med / 1e3, bytes / med / 1e3 / 80.0);
   }
+  CK(hipFree(in));
+  CK(hipFree(out));
+  CK(hipStreamDestroy(s));
   return 0;
+}
+
+int main(int argc, char **argv) {
+  const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
+  // 1 GiB of data per geometry: Storb's 8 / 32 / 128 MiB chunks
+  int rc = run<64, 96>(rounds, 2u << 20, 8);
+  if (!rc) rc = run<32, 48>(rounds, 1u << 20, 32);
+  if (!rc) rc = run<16, 24>(rounds, 512u << 10, 128);
+  return rc;
 }
