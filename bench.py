@@ -254,34 +254,48 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
                 ctx.encode_chunks_hashed(k, n, host, chunk_bytes, nchunks, out=out, hashes=ids)
             res["hashed"] = round(reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0),
                                   3)
-        if mode == "pageable" and erased:
+        if erased:
             # download side: every chunk lost `erased`, rebuilt from the first
-            # k survivors (storb_rs_decode_chunks), host shares in, chunks out
+            # k survivors (storb_rs_decode_chunks), host shares in, chunks out;
+            # page-locked shares and output: the kernel reads and writes them
+            # in place (zero-copy), pageable: staged through pinned buffers
             surv = [i for i in range(n) if i not in erased][:k]
             par = out.reshape(nchunks, n - k, B)
             dat = host.reshape(nchunks, k, B)
             chunks = [([dat[c, i] if i < k else par[c, i - k] for i in surv], surv)
                       for c in range(nchunks)]
-            rec = np.empty((nchunks, chunk_bytes), np.uint8)
+            if mode == "pinned":
+                rbuf = _lib.PinnedBuffer(nchunks * chunk_bytes)
+                rec = rbuf.array.reshape(nchunks, chunk_bytes)
+            else:
+                rec = np.empty((nchunks, chunk_bytes), np.uint8)
+            rec[:] = 0
             ctx.decode_chunks(k, n, B, 0, chunks, out=rec)  # warm
             if not np.array_equal(rec.reshape(-1), host):
-                raise SystemExit("host decode_chunks round trip mismatch")
+                raise SystemExit(f"host decode_chunks round trip mismatch ({mode})")
             t0 = time.perf_counter()
             for _ in range(reps):
                 ctx.decode_chunks(k, n, B, 0, chunks, out=rec)
-            res["decode"] = round(reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0), 3)
+            res["decode" if mode == "pageable" else "decode_pinned"] = round(
+                reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0), 3)
+            if mode == "pinned":
+                rec = None
+                rbuf.free()
         if mode == "pinned":
             src.free()
             dst.free()
     return {"value": res["pageable"], "unit": "GiB/s", "pinned_value": res["pinned"],
-            "decode_value": res.get("decode"), "hashed_value": res.get("hashed"),
+            "decode_value": res.get("decode"), "decode_pinned_value": res.get("decode_pinned"),
+            "hashed_value": res.get("hashed"),
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB host chunks "
                     "-> H2D -> encode -> D2H parity, 2 streams; value = pageable caller "
                     "buffers (staged), pinned_value = page-locked caller buffers (zero-copy kernels); "
                     "hashed_value = storb_rs_encode_chunks_hashed (parity + every share's blake3 "
                     "id computed on the GPU), pageable; "
                     f"decode_value = storb_rs_decode_chunks of the same chunks with shares "
-                    f"{sorted(erased)} lost (host shares in, chunks out)"}
+                    f"{sorted(erased)} lost (host shares in, chunks out), pageable; "
+                    "decode_pinned_value = the same from page-locked shares into a page-locked "
+                    "output (zero-copy decode kernels, no host copies)"}
 
 
 def shard_hash_rate(ctx, w, stream, reps=3):

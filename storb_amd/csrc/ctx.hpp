@@ -178,6 +178,8 @@ int next_round_robin();
 void blake3_host(const uint8_t *data, size_t len, uint8_t out[32]);
 // [p, p+len) inside one storb_rs_host_alloc / _register range.
 bool range_pinned(const void *p, size_t len);
+// Base of the registered / allocated page-locked range holding [p, p+len), or null.
+const uint8_t *pinned_base(const void *p, size_t len);
 Variant pick_variant(const storb_rs_ctx *ctx);
 // Device tables of a rows x k coefficient matrix (cached per context), made
 // ready for launches on stream s; call tables_used() after those launches.

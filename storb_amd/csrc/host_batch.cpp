@@ -192,6 +192,7 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   if (out_stride < outlen) return fail(ctx, STORB_RS_EINVAL, "decode_chunks: out_stride < chunk");
   // per chunk: its k slot shares (pointers) and erasure pattern
   std::vector<const uint8_t *> slot_ptr(static_cast<size_t>(nchunks) * k);
+  std::vector<uint8_t> slot_is_data(static_cast<size_t>(nchunks) * k);  // slot s holds share s
   std::map<std::vector<uint32_t>, std::vector<uint32_t>> groups;
   std::vector<uint32_t> plain;
   size_t off = 0;
@@ -204,6 +205,7 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
     }
     for (uint32_t s = 0; s < k; s++) {
       slot_ptr[static_cast<size_t>(c) * k + s] = shares[off + slot_pos[s]];
+      slot_is_data[static_cast<size_t>(c) * k + s] = slot_idx[s] == s;
       if (!slot_ptr[static_cast<size_t>(c) * k + s])
         return fail(ctx, STORB_RS_EINVAL, "decode_chunks: null share");
     }
@@ -226,6 +228,130 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
       for (uint32_t s = 0; s < k; s++)
         put_row(plain[i], s, slot_ptr[static_cast<size_t>(plain[i]) * k + s]);
     });
+  if (groups.empty()) return STORB_RS_OK;
+
+  // Zero-copy groups: page-locked caller shares AND output (storb_rs_host_alloc
+  // / _register), no padding, 16-B aligned. The decode kernel reads the k
+  // survivors over PCIe where they lie and writes the rebuilt rows and the
+  // surviving data shares (fused assembly) straight into `out`: no host copy
+  // at all, where the staged path below copies 2 k B per chunk on the host
+  // (survivors into staging, present shares into out) and is bound by it.
+  // Chunks of a group whose share pointers advance by one constant per slot
+  // (an arena of equal chunks) share a launch; others get one launch each.
+  const bool zc_out = ctx->zc_batch && padlen == 0 && block % kAlign == 0 &&
+                      out_stride % kAlign == 0 && reinterpret_cast<uintptr_t>(out) % kAlign == 0 &&
+                      range_pinned(out, static_cast<size_t>(nchunks - 1) * out_stride + outlen);
+  auto share_zc = [&](uint32_t c) {
+    for (uint32_t sl = 0; sl < k; sl++) {
+      const uint8_t *p = slot_ptr[static_cast<size_t>(c) * k + sl];
+      if (reinterpret_cast<uintptr_t>(p) % kAlign || !range_pinned(p, block)) return false;
+    }
+    return true;
+  };
+  // Device address of a page-locked pointer: one hipHostGetDevicePointer per
+  // registered range (a range maps linearly), not one per share.
+  std::map<const uint8_t *, uint8_t *> dev_base;
+  auto dev_ptr = [&](const uint8_t *p, size_t len, uint8_t **d) -> hipError_t {
+    const uint8_t *b = pinned_base(p, len);
+    if (!b) return hipErrorInvalidValue;
+    auto f = dev_base.find(b);
+    if (f == dev_base.end()) {
+      uint8_t *db = nullptr;
+      const hipError_t e = host_dev_ptr(const_cast<uint8_t *>(b), &db);
+      if (e != hipSuccess) return e;
+      f = dev_base.emplace(b, db).first;
+    }
+    *d = f->second + (p - b);
+    return hipSuccess;
+  };
+  // Who assembles the surviving data shares into `out` on the zero-copy path:
+  // the host copy pool while the kernels run (default: PCIe then carries only
+  // the k survivors in and the e rebuilt rows out), or the kernel itself
+  // (STORB_RS_ZC_ASSEMBLY=kernel: fused assembly, k rows out over PCIe).
+  static const bool host_assembly = [] {
+    const char *e = std::getenv("STORB_RS_ZC_ASSEMBLY");
+    return !(e && std::strcmp(e, "kernel") == 0);
+  }();
+  std::vector<uint32_t> zc_chunks;  // chunks whose present data shares the host copies
+  DeviceGuard dg(ctx->device);
+  uint32_t zc_launches = 0;
+  for (auto it = groups.begin(); zc_out && it != groups.end();) {
+    const std::vector<uint32_t> &slots = it->first, &cs = it->second;
+    bool ok = true;
+    for (uint32_t c : cs) ok = ok && share_zc(c);
+    if (!ok) {
+      ++it;
+      continue;
+    }
+    std::vector<uint8_t> coef;
+    std::vector<uint32_t> missing;
+    int rc = decode_rows(ctx, k, n, slots, coef, missing);
+    if (rc) return rc;
+    const uint32_t e = static_cast<uint32_t>(missing.size());
+    auto sp = [&](uint32_t c, uint32_t sl) { return slot_ptr[static_cast<size_t>(c) * k + sl]; };
+    // chunk i + 1 continues the run of chunk i with steps (dc, dp[])
+    auto step_ok = [&](size_t i, uint32_t dc, const std::vector<uintptr_t> &dp) {
+      if (cs[i + 1] - cs[i] != dc) return false;
+      for (uint32_t sl = 0; sl < k; sl++)
+        if (reinterpret_cast<uintptr_t>(sp(cs[i + 1], sl)) - reinterpret_cast<uintptr_t>(sp(cs[i], sl)) != dp[sl])
+          return false;
+      return true;
+    };
+    for (size_t i = 0; i < cs.size();) {
+      size_t j = i + 1;
+      uint32_t dc = 0;
+      std::vector<uintptr_t> dp(k, block);
+      if (j < cs.size()) {
+        dc = cs[j] - cs[i];
+        bool fwd = true;  // strides are unsigned and kept 16-B aligned
+        for (uint32_t sl = 0; sl < k; sl++) {
+          dp[sl] = reinterpret_cast<uintptr_t>(sp(cs[j], sl)) - reinterpret_cast<uintptr_t>(sp(cs[i], sl));
+          fwd = fwd && reinterpret_cast<uintptr_t>(sp(cs[j], sl)) > reinterpret_cast<uintptr_t>(sp(cs[i], sl)) &&
+                dp[sl] % kAlign == 0;
+        }
+        if (fwd)
+          while (j < cs.size() && step_ok(j - 1, dc, dp)) j++;
+        else
+          dp.assign(k, block);
+      }
+      const uint32_t cn = static_cast<uint32_t>(j - i);
+      uint8_t *obase = out + static_cast<size_t>(cs[i]) * out_stride;
+      // (one chunk: any pitch >= a share does; copy-first assembly needs one)
+      const size_t ostr = cn > 1 ? static_cast<size_t>(dc) * out_stride : outlen;
+      std::vector<const uint8_t *> in(k);
+      std::vector<size_t> ins(k);
+      std::vector<uint8_t *> cp(k, nullptr), o(e);
+      std::vector<size_t> cps(k, ostr), outs(e, ostr);
+      for (uint32_t sl = 0; sl < k; sl++) {
+        uint8_t *d = nullptr;
+        HIP_TRY(ctx, dev_ptr(sp(cs[i], sl), block, &d));
+        in[sl] = d;
+        ins[sl] = cn > 1 ? dp[sl] : block;
+        if (slots[sl] == sl && !host_assembly)  // present data share: assembled by the kernel
+          HIP_TRY(ctx, dev_ptr(obase + static_cast<size_t>(sl) * block, block, &cp[sl]));
+      }
+      for (uint32_t r = 0; r < e; r++)
+        HIP_TRY(ctx, dev_ptr(obase + static_cast<size_t>(missing[r]) * block, block, &o[r]));
+      rc = apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), block, cn,
+                 ctx->pipe[zc_launches++ & 1], host_assembly ? nullptr : cp.data(), cps.data());
+      if (rc) return rc;
+      i = j;
+    }
+    if (host_assembly) zc_chunks.insert(zc_chunks.end(), cs.begin(), cs.end());
+    it = groups.erase(it);
+  }
+  if (!zc_chunks.empty()) {  // overlaps the kernels (disjoint rows of out)
+    std::vector<std::pair<uint32_t, uint32_t>> rows;  // (chunk, present data slot)
+    for (uint32_t c : zc_chunks)
+      for (uint32_t sl = 0; sl < k; sl++)
+        if (slot_is_data[static_cast<size_t>(c) * k + sl]) rows.emplace_back(c, sl);
+    pool.run(static_cast<int>(rows.size()), [&](int i) {
+      put_row(rows[i].first, rows[i].second,
+              slot_ptr[static_cast<size_t>(rows[i].first) * k + rows[i].second]);
+    });
+  }
+  if (zc_launches)
+    for (int b = 0; b < 2; b++) HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[b]));
   if (groups.empty()) return STORB_RS_OK;
 
   struct Item {
@@ -253,7 +379,6 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   }
   batch = 0;
   for (auto &it : items) batch = std::max(batch, it.cn);
-  DeviceGuard dg(ctx->device);
   for (int b = 0; b < 2; b++) {
     HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
     HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(emax) * S * batch));

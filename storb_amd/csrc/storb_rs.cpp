@@ -56,14 +56,17 @@ int next_round_robin() { return g_rr.fetch_add(1); }
 static std::mutex g_pin_mu;
 static std::map<uintptr_t, std::pair<size_t, bool>> g_pinned;  // base -> (len, allocated here)
 
-bool range_pinned(const void *p, size_t len) {
-  if (!p || len == 0) return false;
+bool range_pinned(const void *p, size_t len) { return pinned_base(p, len) != nullptr; }
+
+const uint8_t *pinned_base(const void *p, size_t len) {
+  if (!p || len == 0) return nullptr;
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   std::lock_guard<std::mutex> lk(g_pin_mu);
   auto it = g_pinned.upper_bound(a);
-  if (it == g_pinned.begin()) return false;
+  if (it == g_pinned.begin()) return nullptr;
   --it;
-  return a - it->first + len <= it->second.first;
+  return a - it->first + len <= it->second.first ? reinterpret_cast<const uint8_t *>(it->first)
+                                                  : nullptr;
 }
 
 

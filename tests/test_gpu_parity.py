@@ -232,6 +232,61 @@ def test_host_decode_chunks_batch(ctx):
     assert e.value.code == _lib.ENOTENOUGH
 
 
+@pytest.mark.parametrize("zc", [True, False])
+def test_host_decode_chunks_page_locked(zc, monkeypatch):
+    """storb_rs_decode_chunks with page-locked shares and output (the
+    download path with receive buffers from storb_rs_host_alloc): the decode
+    kernel reads the survivors over PCIe in place and writes rebuilt rows and
+    surviving data shares straight into the output (STORB_RS_ZC_BATCH=1,
+    default), or the staged pipeline (=0). Shares in an arena with regular
+    strides (one launch per run of chunks), scattered shares (one launch per
+    chunk), a pageable share in one chunk (that pattern's group is staged),
+    and padded chunks (staged: the last row is truncated). Oracle-exact."""
+    monkeypatch.setenv("STORB_RS_ZC_BATCH", "1" if zc else "0")
+    c = _lib.Context(0)
+    rng = random.Random(5)
+    for k, n, B, cnt, pad in [(4, 6, 256 << 10, 12, 0), (16, 24, 512 << 10, 6, 0),
+                              (8, 12, 64 << 10, 9, 0), (4, 6, 64 << 10, 5, 3)]:
+        L = k * B - pad
+        data = rnd(L * cnt, 7 * k + B + pad)
+        arena = _lib.PinnedBuffer(cnt * n * B)
+        A = arena.array.reshape(cnt, n, B)
+        for ch in range(cnt):
+            shares, b, p = coracle.encode(k, n, data[ch * L:(ch + 1) * L])
+            assert (b, p) == (B, pad)
+            A[ch] = shares
+        out = _lib.PinnedBuffer(cnt * L)
+        lost = [0, 1] if k > 2 else [0]
+        pattern = [i for i in range(n) if i not in lost][:k]
+        scratch = _lib.PinnedBuffer(cnt * n * B)
+        slots = scratch.array.reshape(cnt * n, B)
+        for layout in ("arena", "scattered", "mixed"):
+            perm = rng.sample(range(cnt * n), cnt * n)       # share (ch, i) -> scratch slot
+            chunks = []
+            for ch in range(cnt):
+                ids = list(pattern)
+                if ch % 3 == 2:
+                    ids = list(range(n - k, n))              # another pattern
+                if layout == "arena":
+                    shares = [A[ch, i] for i in ids]
+                else:
+                    shares = []
+                    for i in ids:
+                        slots[perm[ch * n + i]] = A[ch, i]
+                        shares.append(slots[perm[ch * n + i]])
+                if layout == "mixed" and ch == 1:
+                    shares[0] = np.array(shares[0])          # pageable copy
+                chunks.append((shares, ids))
+            o = out.array[:cnt * L].reshape(cnt, L)
+            o[:] = 0x5A
+            got = c.decode_chunks(k, n, B, pad, chunks, out=o)
+            for ch in range(cnt):
+                assert np.array_equal(got[ch], data[ch * L:(ch + 1) * L]), (k, n, layout, ch)
+        for buf in (arena, scratch, out):
+            buf.free()
+    c.close()
+
+
 # ----------------------------------------------------------- device API
 def dev_encode_check(ctx, k, n, B, ns, kernel=_lib.KERNEL_PERM, offset=0):
     ctx.set_kernel(kernel)
