@@ -4,7 +4,8 @@ the CPU oracle (test infrastructure: the oracle is the checker only).
 
 Each round draws a geometry ((k, n) from Storb's sizings plus odd ones), a
 chunk length (1 byte .. 6 MiB, ragged), an entry point (single encode /
-decode / repair, batched encode_chunks[_hashed] / decode_chunks, device
+decode / repair, batched encode_chunks[_hashed] / decode_chunks (page-locked:
+scattered or arena shares, decoded in place), device
 batched encode / decode / repair) and page-locked or pageable buffers, and
 compares the result byte for byte with the oracle. Runs for --seconds and
 prints one JSON line; exits non-zero on the first mismatch.
@@ -108,12 +109,24 @@ def one(ctx, rng, stats):
         cnt = rng.randint(1, max(1, min(24, (32 << 20) // max(L, 1))))
         objs = [data] + [rnd(rng, L) for _ in range(cnt - 1)]
         batch = []
-        for o in objs:
+        arena = pin and rng.random() < 0.5  # every chunk's shares at one stride
+        if arena:
+            ar = pinned_copy(np.zeros(cnt * n * B, np.uint8), keep).reshape(cnt, n, B)
+        for c, o in enumerate(objs):
             sh = coracle.encode(k, n, o)[0]
             ids = rng.sample(range(n), rng.randint(k, n))
-            batch.append(([sh[i] for i in ids], ids))
-        got = ctx.decode_chunks(k, n, B, pad, batch)
-        check(all(np.array_equal(got[c], objs[c]) for c in range(cnt)), tag + f" cnt={cnt}")
+            if rng.random() < 0.5:  # several chunks with one erasure pattern
+                ids = list(range(n - k, n))
+            if arena:
+                ar[c] = sh
+                batch.append(([ar[c, i] for i in ids], ids))
+            else:
+                batch.append(([pinned_copy(sh[i], keep) if pin else sh[i] for i in ids], ids))
+        out = (pinned_copy(np.zeros(cnt * L, np.uint8), keep).reshape(cnt, L) if pin
+               else None)
+        got = ctx.decode_chunks(k, n, B, pad, batch, out=out)
+        check(all(np.array_equal(got[c], objs[c]) for c in range(cnt)),
+              tag + f" cnt={cnt} arena={arena}")
     else:
         ns = rng.randint(1, 6)
         Bd = rng.choice([16, 1024, 4096 + 16, 32 << 10, B - B % 16 or 16])
