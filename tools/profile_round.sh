@@ -28,6 +28,7 @@ trace config6_erase16 --config 6 --erase 16
 trace config3 --config 3
 trace config4 --config 4
 trace config7 --config 7
+trace config7_erase32 --config 7 --erase 32
 timeout -k 10 400 python3 bench.py > "$OUT/bench_default.log" 2>&1
 echo "default bench done"
 echo done
