@@ -119,11 +119,10 @@ __device__ __forceinline__ void st_nt(v4 *p, v4 v) {
 #endif
 }
 
-// One share's 32 bytes (already bit-sliced) folded into the R x 8
-// accumulator planes with the Four-Russians tables.
-template <class M, int J>
-__device__ __forceinline__ void fold_planes(uint32_t (&acc)[M::R][8], const uint32_t (&x)[8]) {
-  uint32_t lo[16], hi[16];
+// The Four-Russians tables of one share's 32 bytes (already bit-sliced):
+// lo[m] / hi[m] = XOR of the planes 0-3 / 4-7 selected by the bits of m.
+__device__ __forceinline__ void make_tables(const uint32_t (&x)[8], uint32_t (&lo)[16],
+                                            uint32_t (&hi)[16]) {
   lo[0] = 0;
   hi[0] = 0;
 #pragma unroll
@@ -132,6 +131,12 @@ __device__ __forceinline__ void fold_planes(uint32_t (&acc)[M::R][8], const uint
     lo[m] = rest ? lo[rest] ^ x[b] : x[b];
     hi[m] = rest ? hi[rest] ^ x[4 + b] : x[4 + b];
   }
+}
+
+// Share J's tables folded into the R x 8 accumulator planes.
+template <class M, int J>
+__device__ __forceinline__ void fold_tables(uint32_t (&acc)[M::R][8], const uint32_t (&lo)[16],
+                                            const uint32_t (&hi)[16]) {
 #pragma unroll
   for (int p = 0; p < M::R; p++) {
 #pragma unroll
@@ -146,6 +151,15 @@ __device__ __forceinline__ void fold_planes(uint32_t (&acc)[M::R][8], const uint
         acc[p][b] ^= hi[h];
     }
   }
+}
+
+// One share's 32 bytes (already bit-sliced) folded into the R x 8
+// accumulator planes with the Four-Russians tables.
+template <class M, int J>
+__device__ __forceinline__ void fold_planes(uint32_t (&acc)[M::R][8], const uint32_t (&x)[8]) {
+  uint32_t lo[16], hi[16];
+  make_tables(x, lo, hi);
+  fold_tables<M, J>(acc, lo, hi);
 }
 
 // The loads of one group of G shares: 2 x dwordx4 per share and lane, at the
@@ -255,6 +269,15 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
 // bit-planes through LDS; both waves fold every input into their own rows.
 // One barrier per load group, LDS double-buffered by group parity.
 
+template <bool C, class A, class B>
+struct __type_pick {
+  typedef A type;
+};
+template <class A, class B>
+struct __type_pick<false, A, B> {
+  typedef B type;
+};
+
 // Rows [R0, R1) of matrix M, as a matrix type of their own.
 template <class M, int R0, int R1>
 struct RowSlice {
@@ -279,6 +302,12 @@ template <int G>
 struct SplitLds {
   v4 v[2 * 2 * (G / 2) * 2 * 64];
 };
+// Table-sharing variant (SPLIT_TAB): [group parity][owner wave][G/2 inputs][8 quads][64 lanes],
+// quad q = table entries 4q..4q+3 of lo (q < 4) / hi (q >= 4).
+template <int G>
+struct SplitTabLds {
+  v4 v[2 * 2 * (G / 2) * 8 * 64];
+};
 static_assert(sizeof(SplitLds<2>) == split_lds_bytes(2) && sizeof(SplitLds<4>) == split_lds_bytes(4),
               "rs_args.h split_lds_bytes");
 
@@ -289,7 +318,7 @@ __device__ __forceinline__ void split_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <class M, int G, int W>
+template <class M, int G, int W, bool TAB = false>
 __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t stripe, uint32_t v0,
                                               uint32_t cols, uint32_t lane, v4 *lds) {
   constexpr int K = M::K, R = M::R, H = G / 2, RA = (R + 1) / 2;
@@ -324,10 +353,22 @@ __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t strip
       asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
                    "+v"(x[6]), "+v"(x[7]));
       transpose8(x);
-      v4 *slot = lds + ((((gi & 1) * 2 + W) * H + h) * 2) * 64 + lane;
-      slot[0] = v4{x[0], x[1], x[2], x[3]};
-      slot[64] = v4{x[4], x[5], x[6], x[7]};
-      fold_planes<MW, j>(acc, x);
+      if constexpr (TAB) {
+        uint32_t lo[16], hi[16];
+        make_tables(x, lo, hi);
+        v4 *slot = lds + ((((gi & 1) * 2 + W) * H + h) * 8) * 64 + lane;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          slot[q * 64] = v4{lo[4 * q], lo[4 * q + 1], lo[4 * q + 2], lo[4 * q + 3]};
+          slot[(4 + q) * 64] = v4{hi[4 * q], hi[4 * q + 1], hi[4 * q + 2], hi[4 * q + 3]};
+        }
+        fold_tables<MW, j>(acc, lo, hi);
+      } else {
+        v4 *slot = lds + ((((gi & 1) * 2 + W) * H + h) * 2) * 64 + lane;
+        slot[0] = v4{x[0], x[1], x[2], x[3]};
+        slot[64] = v4{x[4], x[5], x[6], x[7]};
+        fold_planes<MW, j>(acc, x);
+      }
       fence_acc(acc);
     });
     split_barrier();
@@ -335,10 +376,22 @@ __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t strip
     static_for<H>([&](auto HH) {
       constexpr int h = decltype(HH)::value;
       constexpr int j = gi * G + (1 - W) * H + h;
-      const v4 *slot = lds + ((((gi & 1) * 2 + (1 - W)) * H + h) * 2) * 64 + lane;
-      const v4 P = slot[0], Q = slot[64];
-      uint32_t x[8] = {P[0], P[1], P[2], P[3], Q[0], Q[1], Q[2], Q[3]};
-      fold_planes<MW, j>(acc, x);
+      if constexpr (TAB) {
+        const v4 *slot = lds + ((((gi & 1) * 2 + (1 - W)) * H + h) * 8) * 64 + lane;
+        uint32_t lo[16], hi[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const v4 L = slot[q * 64], Hq = slot[(4 + q) * 64];
+          lo[4 * q] = L[0], lo[4 * q + 1] = L[1], lo[4 * q + 2] = L[2], lo[4 * q + 3] = L[3];
+          hi[4 * q] = Hq[0], hi[4 * q + 1] = Hq[1], hi[4 * q + 2] = Hq[2], hi[4 * q + 3] = Hq[3];
+        }
+        fold_tables<MW, j>(acc, lo, hi);
+      } else {
+        const v4 *slot = lds + ((((gi & 1) * 2 + (1 - W)) * H + h) * 2) * 64 + lane;
+        const v4 P = slot[0], Q = slot[64];
+        uint32_t x[8] = {P[0], P[1], P[2], P[3], Q[0], Q[1], Q[2], Q[3]};
+        fold_planes<MW, j>(acc, x);
+      }
       fence_acc(acc);
     });
   });
@@ -356,9 +409,10 @@ __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t strip
 }
 
 // Grid: nstripes x tiles of kSplitColsPerTile columns, kSplitThreads lanes.
-template <class M, int G, int SWZ = 0>
+// TAB: share the Four-Russians tables instead of the planes (tools/k64split.hip A/B).
+template <class M, int G, int SWZ = 0, bool TAB = false>
 __device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
-  __shared__ SplitLds<G> lds;
+  __shared__ typename __type_pick<TAB, SplitTabLds<G>, SplitLds<G>>::type lds;
   constexpr uint32_t CPT = kSplitColsPerTile;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + CPT - 1) / CPT;
@@ -369,9 +423,9 @@ __device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
   const uint32_t v0 = tile * CPT + lane;
   // wave-uniform (an SGPR), so the two row halves are scalar branches
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
-    bs_split_wave<M, G, 0>(a, stripe, v0, cols, lane, lds.v);
+    bs_split_wave<M, G, 0, TAB>(a, stripe, v0, cols, lane, lds.v);
   else
-    bs_split_wave<M, G, 1>(a, stripe, v0, cols, lane, lds.v);
+    bs_split_wave<M, G, 1, TAB>(a, stripe, v0, cols, lane, lds.v);
 }
 
 template <class M, int G, int T = kBsThreads, int SWZ = 0>
