@@ -458,7 +458,7 @@ def leg_kernel_match(a, w, leg):
     if leg in w.jit_legs:
         return f"storb_bs_jit_k{w.k}_r{jit_blocks(w.k, leg_rows(w, leg))[1]}_"
     if leg == "encode":
-        if a.kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48)):
+        if a.kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48), (64, 96)):
             return f"rs_encode_bitslice<{w.k}, {w.n}>"
         k, r = w.k, w.n - w.k
     else:
@@ -544,7 +544,7 @@ def kernel_names(kernel, w):
     names = {}
     table = "lds" if kernel == "lds" else "perm"
     if "encode" in w.legs:
-        bits = kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48))
+        bits = kernel == "auto" and (w.k, w.n) in ((16, 24), (32, 48), (64, 96))
         names["encode"] = (f"rs_encode_bitslice<{w.k},{w.n}>" if bits
                            else jit_name(w, "encode") if "encode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")

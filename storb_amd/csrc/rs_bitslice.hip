@@ -4,14 +4,17 @@
 
 namespace storb_rs {
 
+hipError_t launch_encode_bitslice_64_96(const ApplyArgs &a, hipStream_t s);  // rs_bitslice64.hip
+
 bool bitslice_supported(uint32_t k, uint32_t n) {
-  return (k == 16 && n == 24) || (k == 32 && n == 48);
+  return (k == 16 && n == 24) || (k == 32 && n == 48) || (k == 64 && n == 96);
 }
 
 hipError_t launch_encode_bitslice(const ApplyArgs &a, uint32_t n, hipStream_t s) {
   if (a.r != n - a.k || !vector_ok(a)) return hipErrorInvalidValue;
   if (a.k == 16 && n == 24) return bs::launch_bitslice<16, 24>(a, s);
   if (a.k == 32 && n == 48) return bs::launch_bitslice<32, 48>(a, s);
+  if (a.k == 64 && n == 96) return launch_encode_bitslice_64_96(a, s);
   return hipErrorInvalidValue;
 }
 

@@ -190,8 +190,9 @@ def test_jit_not_used_where_table_kernel_is_hbm_bound(ctx):
 @pytest.mark.timeout(600)
 def test_jit_k64_encode_and_decode(ctx):
     """Storb's widest geometry: objects from ~160 GiB are chunked at 128-256
-    MiB and sized k = 64, m = 96 (piece.rs:292-317). Encode (32 parity rows)
-    and a 20-lost decode (20 rows) each run as ONE row-split launch (two waves
+    MiB and sized k = 64, m = 96 (piece.rs:292-317). Encode (32 parity rows,
+    ahead-of-time kernel) and a 20-lost decode (20 rows, compiled) each run as
+    ONE row-split launch (two waves
     per workgroup, 16 / 10 rows each, every input read once); a ragged share
     size (last tile partly past the share end), a 17-row decode (rows split
     9 + 8), k = 40 (20 parity rows split, 3-lost decode on one wave-size
@@ -215,7 +216,9 @@ def test_jit_k64_encode_and_decode(ctx):
         before = launches()
         ctx.encode_batch_dev(k, n, B, ns, data.data_ptr(), par.data_ptr())
         torch.cuda.synchronize()
-        assert launches() == before + jit_launches(k, n - k), "compiled encode did not run"
+        # (64, 96) has an ahead-of-time row-split encoder (rs_bitslice64.hip): no JIT
+        want = 0 if (k, n) == (64, 96) else jit_launches(k, n - k)
+        assert launches() == before + want, "compiled encode did not run"
         assert np.array_equal(par.cpu().numpy(), par_h), (k, "compiled encode")
         view = data.view(ns, k, B)
         for e in erased:

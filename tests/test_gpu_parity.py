@@ -331,15 +331,17 @@ def test_dev_encode_tiled_large_matrices(ctx, k, n, B, ns):
 
 
 # Storb's wide full-chunk geometries take the bit-sliced encoder under AUTO
-# (rs_bitslice.hpp): one 16-B column, ragged tiles, exact 8 KiB tiles.
-@pytest.mark.parametrize("k,n", [(16, 24), (32, 48)])
+# (rs_bitslice.hpp; (64, 96) as one row-split launch): one 16-B column,
+# ragged tiles, exact 8 KiB tiles.
+@pytest.mark.parametrize("k,n", [(16, 24), (32, 48), (64, 96)])
 @pytest.mark.parametrize("B,ns", [(16, 3), (1040, 4), (8192, 3), (3 * 8192 + 48, 2),
                                   (16 * 1024 + 1024, 2)])
 def test_dev_encode_bitslice_matches_oracle(ctx, k, n, B, ns):
     dev_encode_check(ctx, k, n, B, ns, kernel=_lib.KERNEL_AUTO)
 
 
-@pytest.mark.parametrize("k,n,B,ns", [(16, 24, 512 << 10, 9), (32, 48, 1 << 20, 3)])
+@pytest.mark.parametrize("k,n,B,ns", [(16, 24, 512 << 10, 9), (32, 48, 1 << 20, 3),
+                                      (64, 96, 2 << 20, 2)])
 def test_bitslice_identical_to_table_kernel(ctx, k, n, B, ns):
     """AUTO (bit-sliced) and forced PERM (v_perm tables) encodes agree byte
     for byte on the config-5 share size, splitmix input."""
