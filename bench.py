@@ -109,6 +109,7 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
     prepared = [coracle.encode(k, n, d) for d in sample]
     done = 0
     t0 = time.perf_counter()
+    c0 = time.thread_time()
     while True:
         i = done % len(sample)
         if do_encode:
@@ -123,6 +124,7 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
         if time.perf_counter() - t0 >= seconds:
             break
     el = time.perf_counter() - t0
+    on_cpu = time.thread_time() - c0
     legs = int(do_encode) + int(do_decode)
     what = "+".join(x for x, on in (("encode", do_encode), ("decode", do_decode)) if on)
     return {
@@ -134,6 +136,11 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
                    f"{', erased ' + str(sorted(erased)) if do_decode else ''}), {el:.1f} s, "
                    f"1 thread, scalar table-driven zfec restatement -O2 (oracle/); host "
                    f"{platform.machine()}, {os.cpu_count()} logical CPUs visible"),
+        # CPU time the measuring thread got over the wall time of the sample:
+        # well below 1 means the host descheduled it (the GPU boxes are shared;
+        # the same binary has measured 0.11 and 1.9 GiB/s on different boxes,
+        # DESIGN.md §5)
+        "thread_cpu_over_wall": round(on_cpu / el, 3),
     }
 
 
