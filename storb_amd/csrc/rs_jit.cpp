@@ -80,6 +80,7 @@ struct Entry {
   std::atomic<State> state{Pending};  // read by launching threads without the lock
   std::string src;
   std::string name;  // kernel symbol: storb_bs_jit_k<k>_r<rows>_{ip,asm}
+  int opt = 3;       // -O level (opt_level())
   std::vector<char> code;
   std::string log;
   std::map<int, hipFunction_t> fn;  // per device
@@ -123,7 +124,7 @@ class Jit {
   // when the kernel budget is spent); src() writes the kernel source (symbol
   // `name`), only for a new entry. In Sync mode waits for the compile.
   template <typename Src>
-  std::shared_ptr<Entry> get(const std::string &key, const std::string &name, Src &&src) {
+  std::shared_ptr<Entry> get(const std::string &key, const std::string &name, int opt, Src &&src) {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = entries_.find(key);
     std::shared_ptr<Entry> e;
@@ -134,6 +135,7 @@ class Jit {
       e = std::make_shared<Entry>();
       e->src = src();
       e->name = name;
+      e->opt = opt;
       entries_.emplace(key, e);
       queue_.push_back(e);
       pending_++;
@@ -202,7 +204,7 @@ class Jit {
       const auto t0 = std::chrono::steady_clock::now();
       std::vector<char> code;
       std::string log;
-      const bool ok = compile(e->src, code, log);
+      const bool ok = compile(e->src, e->opt, code, log);
       register_exit_hook();
       const double ms =
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -244,18 +246,19 @@ class Jit {
     std::vector<char> code;
     std::string log;
     compile("extern \"C\" __global__ void storb_jit_warm(unsigned *p) { p[threadIdx.x] = 1u; }\n",
-            code, log);
+            3, code, log);
     register_exit_hook();
   }
 
-  static bool compile(const std::string &src, std::vector<char> &code, std::string &log) {
+  static bool compile(const std::string &src, int opt, std::vector<char> &code, std::string &log) {
     hiprtcProgram prog = nullptr;
     const char *hdrs[] = {kRsArgsH, kRsBitsliceCoreH};
     const char *names[] = {"rs_args.h", "rs_bitslice_core.h"};
     if (hiprtcCreateProgram(&prog, src.c_str(), "storb_bs_jit.hip", 2, hdrs, names) !=
         HIPRTC_SUCCESS)
       return false;
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const std::string o = "-O" + std::to_string(opt);
+    const char *opts[] = {"--offload-arch=gfx950", o.c_str(), "-std=c++17"};
     const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
     size_t n = 0;
     if (hiprtcGetProgramLogSize(prog, &n) == HIPRTC_SUCCESS && n > 1) {
@@ -326,6 +329,25 @@ size_t dynamic_lds(size_t lds) {
     return e && e[0] == '1';
   }();
   return !force_static && lds <= (64u << 10) ? lds : 0;
+}
+
+// -O level of a k-input kernel. -O3 up to k = 16 (sub-second compiles); -O1
+// above, where -O3's middle end costs seconds per new pattern (the calls
+// meanwhile run the table kernel) and buys nothing: the kernels are one
+// straight-line, fully unrolled body whose order the source fixes
+// (static_for, ordering fences), and the backend emits the same code -- k =
+// 64 32-row split 26,507 vs 26,513 instructions, 197 VGPRs both; k = 32 16
+// rows 8,237 vs 8,191, 193 VGPRs. GPU A/B (bench, profiles/r2_jit_opt_ab.txt):
+// k = 32 16-lost and k = 64 32-lost decodes equal (0.2720 / 0.2717 ms, 0.370
+// / 0.368), compiles 1.1 vs 2.8 s and 5-6 vs 11.3 s; at k = 16 -O1 was 1.4-2.3 %
+// slower (decode 0.1910 vs 0.1867 ms) for 0.4 s of compile saved, so -O3 there.
+// STORB_RS_JIT_OPT=0..3 forces a level (A/B).
+int opt_level(uint32_t k) {
+  static const int forced = [] {
+    const char *e = std::getenv("STORB_RS_JIT_OPT");
+    return e && e[0] >= '0' && e[0] <= '3' && !e[1] ? e[0] - '0' : -1;
+  }();
+  return forced >= 0 ? forced : (k > 16 ? 1 : 3);
 }
 
 // Kernel symbol, so profiles tell the compiled kernels apart (bench.py and
@@ -441,7 +463,7 @@ static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *c
   std::memcpy(&key[0], hdr, sizeof(hdr));
   std::memcpy(&key[32], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
-  auto e = J.get(key, kernel_name(k, r, copy_mask),
+  auto e = J.get(key, kernel_name(k, r, copy_mask), opt_level(k),
                  [&] { return source(k, r, coef, copy_mask, group, sh, lds, split); });
   if (e && wait) J.wait_for(*e);
   return e;
