@@ -121,6 +121,24 @@ rs_encode_bitslice(const ApplyArgs a) {
     bs_kernel_body<EncMat<K, N>, C::G, C::T, C::SWZ>(a);
 }
 
+// The row-split form for geometries bs_split leaves to one wave per tile
+// (A/B: STORB_RS_BS_SPLIT=1, rs_bitslice.hip). CAP resident per CU.
+template <int K, int N, int CAP>
+__global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(2))) void
+rs_encode_bitslice_split(const ApplyArgs a) {
+  bs_split_body<EncMat<K, N>, kSplitGroup, 0>(a);
+}
+
+template <int K, int N, int CAP>
+hipError_t launch_bitslice_split(const ApplyArgs &a, hipStream_t s) {
+  const uint64_t cols = a.block >> 4;
+  const uint64_t blocks = ((cols + kSplitColsPerTile - 1) / kSplitColsPerTile) * a.nstripes;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+  return launch_lds<rs_encode_bitslice_split<K, N, CAP>>(
+      blocks, kSplitThreads, cap_lds(wg_cap(CAP), split_lds_bytes(kSplitGroup)), s, a);
+}
+
 template <int K, int N>
 hipError_t launch_bitslice(const ApplyArgs &a, hipStream_t s) {
   using C = BsTune<K, N>;
