@@ -428,15 +428,20 @@ class Context:
         return par[:nchunks * (n - k) * B], hashes
 
     def decode_chunks(self, k: int, n: int, block: int, padlen: int, chunks,
-                      out: Optional[np.ndarray] = None) -> np.ndarray:
+                      out: Optional[np.ndarray] = None,
+                      out_stride: Optional[int] = None) -> np.ndarray:
         """Batch of download-side reconstructions: chunks[c] = (shares, idx),
         shares[i] (block bytes) being share idx[i] of chunk c. Returns
-        [nchunks, k*block - padlen] (decode_chunk per chunk, piece.rs:363-387)."""
+        [nchunks, k*block - padlen] (decode_chunk per chunk, piece.rs:363-387).
+        out_stride: bytes between chunks in `out` (default: packed)."""
         nch = len(chunks)
         outlen = k * block - padlen
+        stride = outlen if out_stride is None else int(out_stride)
+        assert stride >= outlen
         if out is None:
-            out = np.empty((nch, outlen), dtype=np.uint8)
-        assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= nch * outlen
+            out = np.empty(max(1, (nch - 1) * stride + outlen), dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.flags.c_contiguous
+        assert out.size >= (nch - 1) * stride + outlen if nch else True
         keep, ptrs, idx, cnt = [], [], [], []
         for shares, ids in chunks:
             assert len(shares) == len(ids)
@@ -451,9 +456,12 @@ class Context:
         I = (C.c_uint32 * max(1, len(idx)))(*idx)
         N = (C.c_uint32 * max(1, nch))(*cnt)
         rc = lib().storb_rs_decode_chunks(self._h, k, n, block, padlen, nch, P, I, N,
-                                          out.ctypes.data, outlen)
+                                          out.ctypes.data, stride)
         self._check(rc, "storb_rs_decode_chunks")
-        return out.reshape(-1)[:nch * outlen].reshape(nch, outlen)
+        flat = out.reshape(-1)
+        if stride == outlen:
+            return flat[:nch * outlen].reshape(nch, outlen)
+        return np.lib.stride_tricks.as_strided(flat, shape=(nch, outlen), strides=(stride, 1))
 
     # --------------------------------------------------- device buffers
     def encode_batch_dev(self, k: int, n: int, block: int, nstripes: int, d_data: int,

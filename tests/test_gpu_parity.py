@@ -282,6 +282,16 @@ def test_host_decode_chunks_page_locked(zc, monkeypatch):
             got = c.decode_chunks(k, n, B, pad, chunks, out=o)
             for ch in range(cnt):
                 assert np.array_equal(got[ch], data[ch * L:(ch + 1) * L]), (k, n, layout, ch)
+            # a caller stride wider than the chunk (aligned: still zero-copy), gap untouched
+            st = L + 4096
+            wide = _lib.PinnedBuffer((cnt - 1) * st + L)
+            wide.array[:] = 0x77
+            got = c.decode_chunks(k, n, B, pad, chunks, out=wide.array, out_stride=st)
+            for ch in range(cnt):
+                assert np.array_equal(got[ch], data[ch * L:(ch + 1) * L]), (k, n, layout, "wide", ch)
+                if ch + 1 < cnt:
+                    assert (wide.array[ch * st + L:(ch + 1) * st] == 0x77).all()
+            wide.free()
         for buf in (arena, scratch, out):
             buf.free()
     c.close()
