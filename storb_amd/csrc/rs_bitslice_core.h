@@ -270,11 +270,11 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
 // One barrier per load group, LDS double-buffered by group parity.
 
 template <bool C, class A, class B>
-struct __type_pick {
+struct pick_type {
   typedef A type;
 };
 template <class A, class B>
-struct __type_pick<false, A, B> {
+struct pick_type<false, A, B> {
   typedef B type;
 };
 
@@ -412,7 +412,7 @@ __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t strip
 // TAB: share the Four-Russians tables instead of the planes (tools/k64split.hip A/B).
 template <class M, int G, int SWZ = 0, bool TAB = false>
 __device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
-  __shared__ typename __type_pick<TAB, SplitTabLds<G>, SplitLds<G>>::type lds;
+  __shared__ typename pick_type<TAB, SplitTabLds<G>, SplitLds<G>>::type lds;
   constexpr uint32_t CPT = kSplitColsPerTile;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + CPT - 1) / CPT;
