@@ -252,15 +252,14 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
             ctx.encode_chunks(k, n, host, chunk_bytes, nchunks, out=out)
         el = time.perf_counter() - t0
         res[mode] = round(reps * nchunks * chunk_bytes / GIB / el, 3)
-        if mode == "pageable":
-            # upload path with Storb's piece ids (upload.rs:623) hashed on the GPU
-            ids = np.zeros((nchunks, n, 32), np.uint8)
+        # upload path with Storb's piece ids (upload.rs:623) hashed on the GPU
+        ids = np.zeros((nchunks, n, 32), np.uint8)
+        ctx.encode_chunks_hashed(k, n, host, chunk_bytes, nchunks, out=out, hashes=ids)
+        t0 = time.perf_counter()
+        for _ in range(reps):
             ctx.encode_chunks_hashed(k, n, host, chunk_bytes, nchunks, out=out, hashes=ids)
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                ctx.encode_chunks_hashed(k, n, host, chunk_bytes, nchunks, out=out, hashes=ids)
-            res["hashed"] = round(reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0),
-                                  3)
+        res["hashed" if mode == "pageable" else "hashed_pinned"] = round(
+            reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0), 3)
         if erased:
             # download side: every chunk lost `erased`, rebuilt from the first
             # k survivors (storb_rs_decode_chunks), host shares in, chunks out;
@@ -293,12 +292,13 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
             dst.free()
     return {"value": res["pageable"], "unit": "GiB/s", "pinned_value": res["pinned"],
             "decode_value": res.get("decode"), "decode_pinned_value": res.get("decode_pinned"),
-            "hashed_value": res.get("hashed"),
+            "hashed_value": res.get("hashed"), "hashed_pinned_value": res.get("hashed_pinned"),
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB host chunks "
                     "-> H2D -> encode -> D2H parity, 2 streams; value = pageable caller "
                     "buffers (staged), pinned_value = page-locked caller buffers (zero-copy kernels); "
                     "hashed_value = storb_rs_encode_chunks_hashed (parity + every share's blake3 "
-                    "id computed on the GPU), pageable; "
+                    "id computed on the GPU), pageable; hashed_pinned_value = the same from "
+                    "page-locked chunks (read in place by the encode kernel); "
                     f"decode_value = storb_rs_decode_chunks of the same chunks with shares "
                     f"{sorted(erased)} lost (host shares in, chunks out), pageable; "
                     "decode_pinned_value = the same from page-locked shares into a page-locked "
