@@ -200,6 +200,7 @@ def test_jit_k64_encode_and_decode(ctx):
     Oracle-exact; the compiles (several seconds each at k = 64) are waited
     for first."""
     for k, n, B, ns, erased in [(64, 96, 16 << 10, 4, list(range(20))),
+                                (64, 96, 16 << 10, 4, list(range(32))),   # every parity used
                                 (64, 96, (16 << 10) + 48, 4, list(range(3, 37, 2))),
                                 (40, 60, 32 << 10, 4, [0, 3, 33]),
                                 (41, 62, 16 << 10, 6, list(range(17)))]:
