@@ -106,7 +106,8 @@ def test_no_device_is_an_error_not_a_fallback():
 def test_jit_compiles_decode_kernels_without_gpu():
     """The run-time-compiled decode kernels build with hipRTC on the host
     (no GPU): RS(16,8) with every data share lost, in place and assembled,
-    and RS(32,16) with 16 lost. Matrices the policy does not want (RS(4,2),
+    RS(32,16) with 16 lost, k = 40 with 3 and with 18 lost (row-split).
+    Matrices the policy does not want (RS(4,2),
     RS(8,4) with 3 lost, one lost share at k = 16) queue nothing."""
     from storb_amd import _lib
     before = _lib.jit_stats()
@@ -121,9 +122,12 @@ def test_jit_compiles_decode_kernels_without_gpu():
     # k > 32 (Storb's k = 64 for objects from ~160 GiB; a short last chunk
     # any k up to 64): one launch sees every input
     _lib.jit_prepare_decode(40, 60, [x for x in range(60) if x not in (1, 7, 30)])
+    # 18 lost rows: one row-split kernel (two waves sharing planes through
+    # LDS, rs_bitslice_core.h bs_split_body), with fused assembly
+    _lib.jit_prepare_decode(40, 60, list(range(18, 60)), assemble=True)
     st = _lib.jit_stats()
     assert st["failed"] == 0 and st["pending"] == 0
-    assert st["compiled"] == before["compiled"] + 4
+    assert st["compiled"] == before["compiled"] + 5
     # the same pattern again is a cache hit
     _lib.jit_prepare_decode(16, 24, list(range(8, 24)))
     assert _lib.jit_stats()["compiled"] == st["compiled"]
