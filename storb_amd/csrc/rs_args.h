@@ -84,9 +84,12 @@ constexpr unsigned bs_cols_per_tile(int threads) { return 2u * static_cast<unsig
 struct BsShape {
   int threads, swz, cap;
 };
+// k > 32 with few rows (Storb's k = 64 decode with a few miners lost): 2 per
+// CU -- bench --config 7 decode (2 lost) 0.1805 ms at 3 per CU -> 0.1744 at
+// 2, 0.1958 at 4 (profiles/r2_k64/shape_c7_ab.txt).
 constexpr BsShape bs_shape(int K, int R) {
   return K <= 16 ? (R >= 6 ? BsShape{64, 1, 6} : BsShape{128, 0, 3})
-                 : (R >= 8 ? BsShape{128, 0, 4} : BsShape{128, 0, 3});
+                 : (R >= 8 ? BsShape{128, 0, 4} : (K > 32 ? BsShape{128, 0, 2} : BsShape{128, 0, 3}));
 }
 
 // Shares per load group (R x 8 accumulators + 2 x G x 8 loaded dwords + 30
