@@ -40,9 +40,14 @@ import platform
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
+# RCCL across rank processes needs dmabuf IPC, the only kind the host driver
+# supports. Set before torch (and HIP) load, so ranks started by
+# torch.distributed.run get it as well as the ones storb_amd/launch.py spawns.
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -55,7 +60,7 @@ METRIC = "GiB/s device-resident RS encode+decode, 1 MiB chunks k=4 m=2, at 1/2/4
 SEED_BASE = 0x5709B
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
@@ -91,7 +96,11 @@ def parse():
                    help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal of the "
                         "multi-rank logic with several ranks on one GPU, see "
                         "STORB_BENCH_DEVICE)")
-    return p.parse_args()
+    p.add_argument("--force-pg", action="store_true",
+                   help="create the process group even at world size 1, so a one-GPU box "
+                        "runs exactly the multi-rank sequence (init_process_group with "
+                        "device_id, all_gather_object, device all_reduce, barrier)")
+    return p.parse_args(argv)
 
 
 def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=True):
@@ -303,6 +312,108 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
                     f"{sorted(erased)} lost (host shares in, chunks out), pageable; "
                     "decode_pinned_value = the same from page-locked shares into a page-locked "
                     "output (zero-copy decode kernels, no host copies)"}
+
+
+def _contention_probe(seconds=0.05):
+    """CPU the measuring thread gets over wall time on a pure host loop (numpy
+    XOR over 4 MiB): well below 1 means the host descheduled it, and any
+    per-call latency measured beside it is inflated."""
+    a = np.arange(1 << 22, dtype=np.uint8)
+    b = np.empty_like(a)
+    t0, c0, it = time.perf_counter(), time.thread_time(), 0
+    while time.perf_counter() - t0 < seconds:
+        np.bitwise_xor(a, 0x5A, out=b)
+        it += 1
+    wall = time.perf_counter() - t0
+    return round((time.thread_time() - c0) / wall, 3), round(it * a.size / wall / 1e9, 2)
+
+
+def shim_path_rate(ctx, seconds=0.4):
+    """The drop-in path as Storb reaches it. The unchanged piece.rs calls
+    Fec::encode / Fec::decode once per chunk (piece.rs:328-329,383-386), which
+    the zfec-rs shim maps onto storb_rs_encode / storb_rs_decode with
+    pageable Vec buffers (integration/zfec-rs-mi355x/src/lib.rs:142-186).
+    One thread, one chunk per call, Storb's own sizing of three object sizes
+    (upload.rs:209 chunking, piece.rs:307-317 k and m). Two figures per call:
+    `call` = the C call alone on pageable caller buffers; `shim` = what
+    lib.rs does around it too (m fresh zeroed Vecs, the k data shares copied
+    out of the chunk; decode: a fresh output Vec). Median per-call latency;
+    decode loses data shares 0.. (2 at most) and gets the first k survivors
+    by index, as decode_chunk hands them over (piece.rs:368-381)."""
+    L = _lib.lib()
+    res = {"what": "per-chunk storb_rs_encode / storb_rs_decode from one thread, pageable "
+                   "buffers, as the zfec-rs shim calls them (lib.rs:142-186)"}
+    cpu_ratio, xor_gbs = _contention_probe()
+    res["host_probe"] = {"thread_cpu_over_wall": cpu_ratio, "numpy_xor_GBps": xor_gbs}
+    rows = []
+    for obj, chunk in ((1 << 20, 256 << 10), (16 << 20, 1 << 20), (1 << 30, 8 << 20)):
+        k, n = _lib.get_k_and_m(chunk)
+        B = -(-chunk // k)
+        data = np.frombuffer(np.random.default_rng(chunk).bytes(chunk), dtype=np.uint8).copy()
+        par = [np.zeros(B, np.uint8) for _ in range(n - k)]
+        pp = (_lib.vp * (n - k))(*[x.ctypes.data for x in par])
+        bo, po = _lib.sz(), _lib.sz()
+        lost = list(range(min(2, n - k)))
+        surv = [i for i in range(n) if i not in lost][:k]
+        row = {"object_bytes": obj, "chunk_bytes": chunk, "k": k, "m_total": n,
+               "lost": lost, "survivors": surv}
+
+        def enc_call():
+            rc = L.storb_rs_encode(ctx.handle, k, n, data.ctypes.data, chunk, pp,
+                                   _lib.C.byref(bo), _lib.C.byref(po))
+            if rc:
+                raise SystemExit(f"shim_path: storb_rs_encode rc {rc}")
+
+        def enc_shim():
+            shares = [np.zeros(B, np.uint8) for _ in range(n)]  # vec![0u8; b] x m
+            for j in range(k):
+                shares[j][:B] = data[j * B:(j + 1) * B]
+            ptr = (_lib.vp * (n - k))(*[shares[i].ctypes.data for i in range(k, n)])
+            rc = L.storb_rs_encode(ctx.handle, k, n, data.ctypes.data, chunk, ptr,
+                                   _lib.C.byref(bo), _lib.C.byref(po))
+            if rc:
+                raise SystemExit(f"shim_path: storb_rs_encode rc {rc}")
+
+        enc_call()
+        allsh = [data[j * B:(j + 1) * B].copy() for j in range(k)] + [x.copy() for x in par]
+        sh = [allsh[i] for i in surv]
+        sp_ = (_lib.vp * k)(*[x.ctypes.data for x in sh])
+        ids = (_lib.C.c_uint32 * k)(*surv)
+        out = np.zeros(chunk, np.uint8)
+
+        def dec_call():
+            rc = L.storb_rs_decode(ctx.handle, k, n, sp_, ids, k, B, 0, out.ctypes.data)
+            if rc:
+                raise SystemExit(f"shim_path: storb_rs_decode rc {rc}")
+
+        def dec_shim():
+            o = np.zeros(k * B, np.uint8)  # vec![0u8; k*b - padding]
+            rc = L.storb_rs_decode(ctx.handle, k, n, sp_, ids, k, B, 0, o.ctypes.data)
+            if rc:
+                raise SystemExit(f"shim_path: storb_rs_decode rc {rc}")
+
+        dec_call()
+        if not np.array_equal(out, data):
+            raise SystemExit(f"shim_path: decode round trip mismatch ({k},{n})")
+        for name, f in (("encode_call", enc_call), ("encode_shim", enc_shim),
+                        ("decode_call", dec_call), ("decode_shim", dec_shim)):
+            f()
+            lat = []
+            t0, c0 = time.perf_counter(), time.thread_time()
+            while time.perf_counter() - t0 < seconds or len(lat) < 11:
+                t = time.perf_counter_ns()
+                f()
+                lat.append(time.perf_counter_ns() - t)
+            wall = time.perf_counter() - t0
+            lat.sort()
+            us = lat[len(lat) // 2] / 1e3
+            row[name] = {"median_us": round(us, 2), "p10_us": round(lat[len(lat) // 10] / 1e3, 2),
+                         "GiBps": round(chunk / GIB / (us * 1e-6), 3), "calls": len(lat),
+                         "thread_cpu_over_wall": round((time.thread_time() - c0) / wall, 3)}
+        rows.append(row)
+    res["geometries"] = rows
+    res["sdma_ceiling_GiBps_user"] = 35.5
+    return res
 
 
 def shard_hash_rate(ctx, w, stream, reps=3):
@@ -669,19 +780,59 @@ class Workload:
         return N * (k + e) * B
 
 
-def rank_info(rank, world, local, dev, backend):
+def rank_info(rank, world, local, dev, use_pg):
     """Who ran: every rank's GPU (ordinal + PCI bus) and the process group's
     own rank count, so a scaling line cannot silently be a 1-rank number."""
     props = torch.cuda.get_device_properties(dev)
     me = {"rank": rank, "device": local, "name": props.name,
           "pci_bus": getattr(props, "pci_bus_id", None), "host": platform.node()}
-    if world == 1:
+    if not use_pg:
         return {"world_size": 1, "backend": None, "pg_ranks": 1, "ranks": [me]}
     ranks = [None] * world
     dist.all_gather_object(ranks, me)
     return {"world_size": world, "backend": dist.get_backend(),
             "pg_ranks": dist.get_world_size(), "ranks": ranks,
             "distinct_gpus": len({(r["host"], r["device"]) for r in ranks})}
+
+
+def line_extras(rank, world, minimal, config):
+    """The bounded, untimed extras this rank adds to its line, all run after
+    the last barrier of the timed region. Rank 0 always carries the
+    single-thread CPU baseline (N > 1 lines too: the driver's scaling lines
+    need it beside the GPU figure); the heavier ones (live PMC traffic passes,
+    copy ceiling, threaded CPU baselines, PCIe-inclusive and per-call host
+    rates, hashing, repair) only at world size 1, where no other rank waits."""
+    if rank != 0 or minimal:
+        return set()
+    ex = {"cpu_baseline"}
+    if world > 1:
+        return ex
+    ex |= {"traffic", "copy_ceiling"}
+    if config in (2, 5, 6):
+        ex |= {"cpu_threads", "host_path", "shim_path", "hashing", "repair"}
+    if config == 3:
+        ex.add("assembly")
+    if config == 4:
+        ex.add("storb_faithful")
+    return ex
+
+
+def init_pg(a, world, dev):
+    """One process group per job: RCCL ('nccl') with each rank bound to its
+    GPU, or gloo for the rehearsal with several ranks on one GPU. --force-pg
+    at world size 1 creates a one-rank group so the exact multi-rank sequence
+    runs on a one-GPU box."""
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(launch.free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if a.dist_backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(a.dist_backend)
+    if dist.get_world_size() != world:
+        raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {world}")
 
 
 def main():
@@ -697,14 +848,10 @@ def main():
     # single-GPU box with --dist-backend gloo); by default rank i uses GPU i.
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(a.dist_backend)
-        if dist.get_world_size() != world:
-            raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {world}")
-    ranks = rank_info(rank, world, local, dev, a.dist_backend)
+    use_pg = world > 1 or a.force_pg
+    if use_pg:
+        init_pg(a, world, dev)
+    ranks = rank_info(rank, world, local, dev, use_pg)
 
     ctx = _lib.Context(local)
     ctx.set_kernel({"auto": _lib.KERNEL_AUTO, "perm": _lib.KERNEL_PERM,
@@ -762,7 +909,7 @@ def main():
     each = a.leg_events == "each"
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(legs) + 1)]
           for _ in range(a.steps if each else 0)]
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -777,7 +924,7 @@ def main():
     e_end.record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = e_start.elapsed_time(e_end) / a.steps
@@ -797,7 +944,9 @@ def main():
         stream.synchronize()
     leg_ms = [sum(e[j].elapsed_time(e[j + 1]) for e in ev) / len(ev) for j in range(len(legs))]
     units = w.N * w.chunk * len(legs)  # user bytes per step on this rank
-    if world > 1:
+    mine = {"rank": rank, "elapsed_s": round(elapsed, 6), "gpu_ms_per_step": round(gpu_ms, 4),
+            "units_per_step": units}
+    if use_pg:
         tdev = dev if a.dist_backend == "nccl" else torch.device("cpu")
         t = torch.tensor([elapsed, float(units)], dtype=torch.float64, device=tdev)
         tmax = t[:1].clone()
@@ -805,8 +954,11 @@ def main():
         tsum = t[1:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, units_all = float(tmax.item()), float(tsum.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     else:
         units_all = float(units)
+        per_rank = [mine]
     value = a.steps * units_all / GIB / elapsed
     alg = {leg: w.alg_bytes(leg) for leg in w.legs}
     # algorithmic bytes of one step / GPU time of one step in the timed region
@@ -836,6 +988,7 @@ def main():
             "parallelism": f"independent objects, {world} GPU(s), no collectives",
         },
         "launch": ranks,
+        "per_rank": per_rank,
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -861,46 +1014,50 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not a.minimal:
-        if not a.no_traffic and max(out["roofline"]["launches_per_leg"].values()) > 1:
+    ex = line_extras(rank, world, a.minimal, a.config)
+    if "traffic" in ex and not a.no_traffic:
+        if max(out["roofline"]["launches_per_leg"].values()) > 1:
             out["roofline"]["traffic_source"] = (
                 "not measured: a leg is several compiled launches (row blocks)")
-        elif not a.no_traffic:
-            pmc = pmc_traffic(a, w)
-            out["roofline"].update(pmc)
+        else:
+            out["roofline"].update(pmc_traffic(a, w))
+    if "copy_ceiling" in ex:
         out["roofline"]["copy_ceiling_gbs"] = copy_ceiling(ctx, dev, stream)
-        if a.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.erased), a.cpu_seconds,
-                                               do_encode="encode" in w.legs,
-                                               do_decode="decode" in w.legs)
-            out["cpu_baseline"]["cpu_model"] = cpu_model()
-            if a.config in (2, 5, 6):
-                # the same code on threads over independent
-                # chunks -- at this box's CPU share per GPU (16) and at
-                # nproc (every logical CPU the OS reports; the cgroup quota,
-                # if any, is stated beside it).
-                er = set(w.erased)
-                nch = max(32, (256 << 20) // w.chunk)
-                out["cpu_baseline_threads"] = cpu_baseline_threads(w.k, w.n, w.chunk, er,
-                                                                   threads=16, nchunks=nch)
-                nproc = os.cpu_count() or 1
-                out["cpu_baseline_nproc"] = cpu_baseline_threads(
-                    w.k, w.n, w.chunk, er, threads=nproc, nchunks=max(nch, nproc))
-                out["cpu_baseline_nproc"]["cpu_quota"] = cpu_quota()
-        if not a.no_host_path and a.config in (2, 5, 6):
-            out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
-                                                   nchunks=max(8, (256 << 20) // w.chunk),
-                                                   erased=[e for e in w.erased if e < w.k])
-        if a.config in (2, 5, 6):
-            out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
-            out["repair"] = repair_rate(ctx, w, stream)
-        if a.config == 3:
-            out["assembly"] = config3_assembly(ctx, w, stream)
-        if a.config == 4:
-            out["storb_faithful"] = config4_storb_faithful(ctx, w, stream)
+    if "cpu_baseline" in ex and a.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.erased), a.cpu_seconds,
+                                           do_encode="encode" in w.legs,
+                                           do_decode="decode" in w.legs)
+        out["cpu_baseline"]["cpu_model"] = cpu_model()
+        out["cpu_baseline"]["measured_by"] = f"rank 0 of {world}, after the timed region"
+    if "cpu_threads" in ex and a.cpu_seconds > 0:
+        # the same code on threads over independent chunks -- at
+        # this box's CPU share per GPU (16) and at nproc (every logical CPU the
+        # OS reports; the cgroup quota, if any, is stated beside it).
+        er = set(w.erased)
+        nch = max(32, (256 << 20) // w.chunk)
+        out["cpu_baseline_threads"] = cpu_baseline_threads(w.k, w.n, w.chunk, er,
+                                                           threads=16, nchunks=nch)
+        nproc = os.cpu_count() or 1
+        out["cpu_baseline_nproc"] = cpu_baseline_threads(
+            w.k, w.n, w.chunk, er, threads=nproc, nchunks=max(nch, nproc))
+        out["cpu_baseline_nproc"]["cpu_quota"] = cpu_quota()
+    if "host_path" in ex and not a.no_host_path:
+        out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
+                                               nchunks=max(8, (256 << 20) // w.chunk),
+                                               erased=[e for e in w.erased if e < w.k])
+    if "shim_path" in ex:
+        out["shim_path"] = shim_path_rate(ctx)
+    if "hashing" in ex:
+        out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
+    if "repair" in ex:
+        out["repair"] = repair_rate(ctx, w, stream)
+    if "assembly" in ex:
+        out["assembly"] = config3_assembly(ctx, w, stream)
+    if "storb_faithful" in ex:
+        out["storb_faithful"] = config4_storb_faithful(ctx, w, stream)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -37,3 +37,37 @@ def test_jit_blocks_match_row_split_and_row_blocks(monkeypatch):
     monkeypatch.setenv("STORB_RS_JIT_SPLIT", "0")
     assert bench.jit_blocks(64, 32) == (2, 16)
     assert bench.jit_blocks(64, 20) == (2, 10)
+
+
+def test_line_extras_cpu_baseline_on_every_rank0_line():
+    """VERDICT r2 'next' 1: every N > 1 line carries the CPU baseline (rank 0,
+    after the timed region); only rank 0 prints, and the heavy extras stay at
+    world size 1 where no other rank waits at the closing barrier."""
+    bench = load_bench()
+    for config in (2, 3, 4, 5, 6, 7):
+        for world in (2, 4, 8):
+            ex = bench.line_extras(0, world, False, config)
+            assert ex == {"cpu_baseline"}, (config, world, ex)
+            for r in range(1, world):
+                assert bench.line_extras(r, world, False, config) == set()
+        one = bench.line_extras(0, 1, False, config)
+        assert {"cpu_baseline", "traffic", "copy_ceiling"} <= one
+        assert bench.line_extras(0, 1, True, config) == set()  # --minimal (PMC child runs)
+    assert {"cpu_threads", "host_path", "shim_path"} <= bench.line_extras(0, 1, False, 2)
+
+
+def test_bench_sets_dmabuf_ipc_before_torch():
+    """RCCL ranks started by torch.distributed.run need
+    HSA_ENABLE_IPC_MODE_LEGACY=0 before HIP loads: bench.py sets it ahead of
+    `import torch`."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    i_env = src.index('os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")')
+    i_torch = src.index("import torch")
+    assert i_env < i_torch
+
+
+def test_force_pg_flag_parses():
+    bench = load_bench()
+    a = bench.parse(["--force-pg", "--dist-backend", "nccl"])
+    assert a.force_pg and a.dist_backend == "nccl"
+    assert not bench.parse([]).force_pg
