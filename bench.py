@@ -73,6 +73,13 @@ def parse(argv=None):
     p.add_argument("--erase", type=int, default=None,
                    help="configs 5/6: data shares 0..E-1 lost per chunk for the decode leg "
                         "(default 2); E >= 3 takes the run-time-compiled bit-sliced decode")
+    p.add_argument("--erase-pattern", choices=["fixed", "download"], default="fixed",
+                   help="fixed: every chunk lost the same shares (--erase / the config's set); "
+                        "download: each chunk keeps the first k+1 pieces to arrive from 10 "
+                        "simulated fetch threads (download.rs:363-451, storb_amd/objects.py "
+                        "download_arrivals), seeded, so the survivor set differs per chunk")
+    p.add_argument("--fail", type=float, default=0.0,
+                   help="--erase-pattern download: probability that a piece's miner is lost")
     p.add_argument("--chunks", type=int, default=None, help="chunks per GPU (config 2/3)")
     p.add_argument("--objects", type=int, default=10000, help="total objects (config 4)")
     p.add_argument("--kernel", choices=["auto", "perm", "lds"], default="auto",
@@ -103,7 +110,8 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
-def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=True):
+def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=True,
+                 survivor_sets=None):
     """Reference CPU path (C restatement of zfec, oracle/) on this host.
 
     Single thread, like the reference: upload.rs:418-420 encodes one object's
@@ -114,6 +122,7 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
     from oracle import coracle  # test infrastructure: the baseline, never the product
 
     survivors = [i for i in range(n) if i not in erased][:k]
+    sets = [sorted(x)[:k] for x in survivor_sets] if survivor_sets else [survivors]
     sample = [coracle.splitmix_bytes(SEED_BASE + i, chunk_bytes) for i in range(8)]
     prepared = [coracle.encode(k, n, d) for d in sample]
     done = 0
@@ -126,7 +135,8 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
         else:
             shares, B, pad = prepared[i]
         if do_decode:
-            rec = coracle.decode(k, n, [shares[s] for s in survivors], survivors, B, pad)
+            sv = sets[done % len(sets)]
+            rec = coracle.decode(k, n, [shares[s] for s in sv], sv, B, pad)
             if done < len(sample) and rec != sample[i].tobytes():
                 raise SystemExit("CPU baseline round trip failed")
         done += 1
@@ -142,7 +152,7 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
         "cores": 1,
         "kind": "port",
         "sample": (f"{done} x {what} of {chunk_bytes >> 10} KiB chunks (k={k},n={n}"
-                   f"{', erased ' + str(sorted(erased)) if do_decode else ''}), {el:.1f} s, "
+                   f"{', erased ' + (str(sorted(erased)) if not survivor_sets else 'per chunk (download patterns)') if do_decode else ''}), {el:.1f} s, "
                    f"1 thread, scalar table-driven zfec restatement -O2 (oracle/); host "
                    f"{platform.machine()}, {os.cpu_count()} logical CPUs visible"),
         # CPU time the measuring thread got over the wall time of the sample:
@@ -238,7 +248,7 @@ def copy_ceiling(ctx, dev, stream, nbytes=1 << 30, reps=5):
     return rates
 
 
-def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
+def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=(), sets=None):
     """PCIe-inclusive encode: host bytes in, parity out (pipelined). Two
     figures: from pageable caller memory (staged through the context's pinned
     buffers by host copy threads) and from page-locked caller memory
@@ -293,6 +303,22 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
                 ctx.decode_chunks(k, n, B, 0, chunks, out=rec)
             res["decode" if mode == "pageable" else "decode_pinned"] = round(
                 reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0), 3)
+            if sets:
+                # download side with a different survivor set per chunk (the
+                # first k + 1 pieces to arrive, download.rs:363-451)
+                dl = []
+                for c in range(nchunks):
+                    ids = sets[c % len(sets)]
+                    dl.append(([dat[c, i] if i < k else par[c, i - k] for i in ids], ids))
+                rec[:] = 0
+                ctx.decode_chunks(k, n, B, 0, dl, out=rec)  # warm
+                if not np.array_equal(rec.reshape(-1), host):
+                    raise SystemExit(f"host decode_chunks (download patterns) mismatch ({mode})")
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    ctx.decode_chunks(k, n, B, 0, dl, out=rec)
+                res["decode_download" if mode == "pageable" else "decode_pinned_download"] = round(
+                    reps * nchunks * chunk_bytes / GIB / (time.perf_counter() - t0), 3)
             if mode == "pinned":
                 rec = None
                 rbuf.free()
@@ -301,6 +327,8 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
             dst.free()
     return {"value": res["pageable"], "unit": "GiB/s", "pinned_value": res["pinned"],
             "decode_value": res.get("decode"), "decode_pinned_value": res.get("decode_pinned"),
+            "decode_download_value": res.get("decode_download"),
+            "decode_pinned_download_value": res.get("decode_pinned_download"),
             "hashed_value": res.get("hashed"), "hashed_pinned_value": res.get("hashed_pinned"),
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB host chunks "
                     "-> H2D -> encode -> D2H parity, 2 streams; value = pageable caller "
@@ -311,7 +339,8 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=()):
                     f"decode_value = storb_rs_decode_chunks of the same chunks with shares "
                     f"{sorted(erased)} lost (host shares in, chunks out), pageable; "
                     "decode_pinned_value = the same from page-locked shares into a page-locked "
-                    "output (zero-copy decode kernels, no host copies)"}
+                    "output (zero-copy decode kernels, no host copies); *_download_value = the "
+                    "same two with each chunk's own survivor set (--erase-pattern download)"}
 
 
 def _contention_probe(seconds=0.05):
@@ -488,11 +517,10 @@ def config3_assembly(ctx, w, stream, reps=5):
     its control erasure {9, 10, 11} (parity only: the first 8 survivors are
     the data shares, decode is pure assembly). decode_chunk returns a fresh
     chunk (piece.rs:363-387), so here the decode writes a separate chunk
-    buffer: every data share, present or rebuilt, is written once. Fused =
-    the decode kernel stores the present shares from its own loads (one
-    pass: k*B read + k*B written); copy_first = STORB_RS_FUSED_ASSEMBLY=0,
-    survivors copied with hipMemcpy2DAsync before the kernel rebuilds the
-    missing ones (re-reads the k - e present shares)."""
+    buffer: every data share, present or rebuilt, is written once, stored by
+    the decode kernel from its own loads (fused assembly: k*B read + k*B
+    written). (Copying the survivors first measured 0.503 vs 0.361 ms,
+    profiles/r1_bench_config3_assembly.json.)"""
     k, n, B, N = w.k, w.n, w.B, w.N
     out = torch.empty_like(w.data)
     sp = stream.cuda_stream
@@ -500,29 +528,21 @@ def config3_assembly(ctx, w, stream, reps=5):
     for erased in ([0, 3, 5], [9, 10, 11]):
         surv = [i for i in range(n) if i not in erased][:k]
         row = {"erased": erased, "survivors": surv}
-        for mode in ("fused", "copy_first"):
-            os.environ["STORB_RS_FUSED_ASSEMBLY"] = "1" if mode == "fused" else "0"
 
-            def go():
-                ctx.decode_batch_dev(k, n, B, N, surv, w.dptr, w.pptr, out.data_ptr(),
-                                     stream=sp)
+        def go():
+            ctx.decode_batch_dev(k, n, B, N, surv, w.dptr, w.pptr, out.data_ptr(), stream=sp)
 
-            try:
-                ms = _time_launches(stream, go, reps)
-            finally:
-                os.environ.pop("STORB_RS_FUSED_ASSEMBLY", None)
-            if not torch.equal(out, w.data):
-                raise SystemExit(f"config 3 assembly ({mode}, erased {erased}) mismatch")
-            with torch.cuda.stream(stream):
-                out.zero_()
-            gbs = N * 2 * k * B / (ms * 1e-3) / 1e9
-            row[mode] = {"ms": round(ms, 4),
-                         "GiBps_user": round(N * k * B / GIB / (ms * 1e-3), 1),
-                         "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        ms = _time_launches(stream, go, reps)
+        if not torch.equal(out, w.data):
+            raise SystemExit(f"config 3 assembly (erased {erased}) mismatch")
+        with torch.cuda.stream(stream):
+            out.zero_()
+        gbs = N * 2 * k * B / (ms * 1e-3) / 1e9
+        row["fused"] = {"ms": round(ms, 4), "GiBps_user": round(N * k * B / GIB / (ms * 1e-3), 1),
+                        "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
         res["control" if erased[0] >= k else "erased_data"] = row
     res["what"] = ("decode into a separate chunk buffer (decode_chunk semantics); bytes = "
-                   "k*B read + k*B written per chunk; fused = assembly inside the decode "
-                   "kernel, copy_first = survivors copied before the kernel")
+                   "k*B read + k*B written per chunk; assembly inside the decode kernel")
     return res
 
 
@@ -555,16 +575,17 @@ def config4_storb_faithful(ctx, w, stream, reps=5):
 
 def leg_rows(w, leg):
     """Rows of the matrix a leg applies: parity rows (encode) or lost data
-    shares (decode)."""
-    return w.n - w.k if leg == "encode" else sum(1 for x in w.erased if x < w.k)
+    shares (decode; the most any stripe lost with per-chunk patterns)."""
+    if leg == "encode":
+        return w.n - w.k
+    return max(len(x) for x in w.lost_rows())
 
 
 def jit_blocks(k, rows):
     """Compiled launches of a rows-row matrix and the first launch's rows
-    (rs_jit.cpp): 17-32 rows at even k are one row-split launch
-    (STORB_RS_JIT_SPLIT=0: row blocks instead), otherwise row blocks of <= 16,
-    balanced."""
-    if 16 < rows <= 32 and k % 2 == 0 and os.environ.get("STORB_RS_JIT_SPLIT", "1")[:1] != "0":
+    (rs_jit.cpp): 17-32 rows at even k are one row-split launch, otherwise
+    row blocks of <= 16, balanced."""
+    if 16 < rows <= 32 and k % 2 == 0:
         return 1, rows
     nb = -(-rows // 16)
     return nb, rows // nb
@@ -573,6 +594,8 @@ def jit_blocks(k, rows):
 def leg_kernel_match(a, w, leg):
     """Substring of the rocprofv3 kernel name each leg launches (compiled
     kernels are named storb_bs_jit_k<k>_r<rows>_{ip,asm}, rs_jit.cpp)."""
+    if leg == "decode" and w.sets is not None:
+        return "rs_apply_desc<"
     if leg in w.jit_legs:
         return f"storb_bs_jit_k{w.k}_r{jit_blocks(w.k, leg_rows(w, leg))[1]}_"
     if leg == "encode":
@@ -606,7 +629,8 @@ def pmc_traffic(a, w):
         return {"traffic": None, "traffic_source": "rocprofv3 not found"}
     child = [sys.executable, os.path.abspath(__file__), "--config", str(a.config),
              "--steps", "3", "--warmup", "1", "--minimal", "--no-check", "--kernel", a.kernel,
-             "--objects", str(a.objects)]
+             "--objects", str(a.objects), "--erase-pattern", a.erase_pattern,
+             "--fail", str(a.fail)]
     if a.chunks:
         child += ["--chunks", str(a.chunks)]
     if a.erase is not None:
@@ -634,6 +658,9 @@ def pmc_traffic(a, w):
             shutil.rmtree(d, ignore_errors=True)
     by_leg = {}
     for leg in w.legs:
+        if leg == "decode" and w.sets is not None:
+            by_leg[leg] = None  # several launches of different sizes per leg: not per-launch
+            continue
         sub = leg_kernel_match(a, w, leg)
         f = [v for (kn, c), xs in vals.items() if c == "FETCH_SIZE" and sub in kn for v in xs]
         wr = [v for (kn, c), xs in vals.items() if c == "WRITE_SIZE" and sub in kn for v in xs]
@@ -645,6 +672,9 @@ def pmc_traffic(a, w):
                        "WRITE_SIZE_KiB": wk, "bytes": b,
                        "vs_algorithmic": round(b / w.alg_bytes(leg), 5)}
     first = by_leg[w.legs[0]]
+    if first is None:
+        return {"traffic": None, "traffic_by_leg": by_leg,
+                "traffic_source": "not measured: per-chunk patterns (several launches per leg)"}
     return {"traffic": first["bytes"], "traffic_by_leg": by_leg,
             "traffic_source": (f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a "
                                f"3-step child run of this workload ({time.perf_counter() - t0:.0f}"
@@ -666,7 +696,10 @@ def kernel_names(kernel, w):
         names["encode"] = (f"rs_encode_bitslice<{w.k},{w.n}>" if bits
                            else jit_name(w, "encode") if "encode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")
-    if "decode" in w.legs:
+    if "decode" in w.legs and w.sets is not None:
+        names["decode"] = (f"rs_apply_desc<{min(w.k, 32)},e> (per-stripe descriptors), one "
+                           f"launch per lost-share count e")
+    elif "decode" in w.legs:
         e = sum(1 for x in w.erased if x < w.k)
         names["decode"] = (jit_name(w, "decode") if "decode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{e}>")
@@ -744,6 +777,30 @@ class Workload:
         k, n = self.k, self.n
         self.B = chunk // k
         self.survivors = [i for i in range(n) if i not in self.erased][:k]
+        self.sets = None  # per-chunk collected pieces (--erase-pattern download)
+        self.fixed_erased = list(self.erased)
+        if a.erase_pattern == "download" and "decode" in self.legs:
+            from storb_amd import objects
+            rng = np.random.default_rng(SEED_BASE + rank)
+            sets = []
+            while len(sets) < N:
+                fail = {i for i in range(n) if rng.random() < a.fail} if a.fail > 0 else ()
+                got = objects.download_arrivals(k, n, rng, fail=fail)
+                if len(got) >= k:  # fewer: reconstruct_chunk's Err, that chunk is not decoded
+                    sets.append(got)
+            self.sets = sets
+            self.lost = [[j for j in range(k) if j not in sorted(s_)[:k]] for s_ in sets]
+            self.set_ids, self.set_cnt = _lib.encode_stripe_shares(sets)
+            hist = {}
+            for x in self.lost:
+                hist[len(x)] = hist.get(len(x), 0) + 1
+            self.pattern_stats = {"distinct_patterns": len({tuple(sorted(s_)[:k]) for s_ in sets}),
+                                  "lost_data_shares_histogram": dict(sorted(hist.items())),
+                                  "fail_probability": a.fail, "fetch_threads": 10,
+                                  "latency": "lognormal(0, 0.5) per fetch"}
+            self.erased = "download"
+            self.workload += (f"; decode: per-chunk survivors from simulated download arrivals "
+                              f"({self.pattern_stats['distinct_patterns']} distinct patterns)")
         self.data = torch.empty(N * k * self.B, dtype=torch.uint8, device=dev)
         self.parity = torch.empty(N * (n - k) * self.B, dtype=torch.uint8, device=dev)
         self.dptr, self.pptr = self.data.data_ptr(), self.parity.data_ptr()
@@ -767,15 +824,29 @@ class Workload:
                                   stream=self.sp)
 
     def decode(self):
+        if self.sets is not None:
+            self.ctx.decode_stripes_dev_raw(self.k, self.n, self.B, self.N, self.set_ids,
+                                            self.set_cnt, self.dptr, self.pptr, self.dptr,
+                                            stream=self.sp)
+            return
         self.ctx.decode_batch_dev(self.k, self.n, self.B, self.N, self.survivors, self.dptr,
                                   self.pptr, self.dptr, stream=self.sp)
 
+    def lost_rows(self):
+        """Per stripe, the data shares the decode leg rebuilds."""
+        if self.sets is not None:
+            return self.lost
+        return [[x for x in self.erased if x < self.k]] * self.N
+
     def alg_bytes(self, leg):
         # SURVEY 8(d): encode reads k*B, writes (n-k)*B per stripe; decode with
-        # e erased data shards reads k*B and writes e*B.
+        # e erased data shards reads k*B and writes e*B (stripes with e = 0
+        # are not touched by an in-place decode).
         k, n, B, N = self.k, self.n, self.B, self.N
         if leg == "encode":
             return N * n * B
+        if self.sets is not None:
+            return sum((k + len(x)) * B for x in self.lost if x)
         e = sum(1 for x in self.erased if x < k)
         return N * (k + e) * B
 
@@ -869,9 +940,14 @@ def main():
         w.encode()
         view = w.data.view(w.N, w.k, w.B)
         with torch.cuda.stream(stream):
-            for e in w.erased:
-                if e < w.k:
-                    view[:, e].zero_()
+            if w.sets is not None:
+                for si, lost in enumerate(w.lost):
+                    for e in lost:
+                        view[si, e].zero_()
+            else:
+                for e in w.erased:
+                    if e < w.k:
+                        view[:, e].zero_()
         w.decode()
         stream.synchronize()
         if not torch.equal(w.data, ref):
@@ -883,8 +959,9 @@ def main():
     # Let it finish so the timed steps run what a steady-state download runs.
     # (Config 7's k = 64 encode runs compiled kernels too.) One pass of every
     # leg queues them; wait for the compiles.
-    for leg in w.legs:
-        getattr(w, leg)()
+    for _ in range(2):  # a matrix is compiled once asked for twice (rs_jit.cpp)
+        for leg in w.legs:
+            getattr(w, leg)()
     stream.synchronize()
     _lib.jit_wait()
     # Which legs run compiled kernels (for the kernel names and the PMC match).
@@ -984,7 +1061,10 @@ def main():
             "baseline_config": a.config,
             "k": w.k, "m_total": w.n, "parity": w.n - w.k, "chunk_bytes": w.chunk,
             "shard_bytes": w.B, "chunks_per_gpu": w.N, "erased": w.erased,
-            "survivors": w.survivors if w.erased else None, "kernel": a.kernel,
+            "erase_pattern": a.erase_pattern,
+            "patterns": getattr(w, "pattern_stats", None),
+            "survivors": w.survivors if w.erased and w.sets is None else None,
+            "kernel": a.kernel,
             "parallelism": f"independent objects, {world} GPU(s), no collectives",
         },
         "launch": ranks,
@@ -1005,8 +1085,10 @@ def main():
                               "separate untimed pass with an event after every leg"),
             "alg_bytes_per_launch": alg,
             "kernel_match": {leg: leg_kernel_match(a, w, leg) for leg in w.legs},
-            "launches_per_leg": {leg: jit_blocks(w.k, leg_rows(w, leg))[0] if leg in w.jit_legs
-                                 else 1 for leg in w.legs},
+            "launches_per_leg": {leg: (len({len(x) for x in w.lost if x})
+                                       if leg == "decode" and w.sets is not None
+                                       else jit_blocks(w.k, leg_rows(w, leg))[0]
+                                       if leg in w.jit_legs else 1) for leg in w.legs},
             "copy_ceiling_gbs": None,
             "jit": {"launches_in_run": jit1["launches"] - jit0["launches"],
                     "compiled": jit1["compiled"], "compile_ms": round(jit1["compile_ms"], 1),
@@ -1016,7 +1098,8 @@ def main():
     }
     ex = line_extras(rank, world, a.minimal, a.config)
     if "traffic" in ex and not a.no_traffic:
-        if max(out["roofline"]["launches_per_leg"].values()) > 1:
+        if any(v > 1 for leg, v in out["roofline"]["launches_per_leg"].items()
+               if not (leg == "decode" and w.sets is not None)):
             out["roofline"]["traffic_source"] = (
                 "not measured: a leg is several compiled launches (row blocks)")
         else:
@@ -1024,16 +1107,17 @@ def main():
     if "copy_ceiling" in ex:
         out["roofline"]["copy_ceiling_gbs"] = copy_ceiling(ctx, dev, stream)
     if "cpu_baseline" in ex and a.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.erased), a.cpu_seconds,
+        out["cpu_baseline"] = cpu_baseline(w.k, w.n, w.chunk, set(w.fixed_erased), a.cpu_seconds,
                                            do_encode="encode" in w.legs,
-                                           do_decode="decode" in w.legs)
+                                           do_decode="decode" in w.legs,
+                                           survivor_sets=w.sets[:64] if w.sets else None)
         out["cpu_baseline"]["cpu_model"] = cpu_model()
         out["cpu_baseline"]["measured_by"] = f"rank 0 of {world}, after the timed region"
     if "cpu_threads" in ex and a.cpu_seconds > 0:
         # the same code on threads over independent chunks -- at
         # this box's CPU share per GPU (16) and at nproc (every logical CPU the
         # OS reports; the cgroup quota, if any, is stated beside it).
-        er = set(w.erased)
+        er = set(w.fixed_erased) if w.sets is None else set(w.lost[0])
         nch = max(32, (256 << 20) // w.chunk)
         out["cpu_baseline_threads"] = cpu_baseline_threads(w.k, w.n, w.chunk, er,
                                                            threads=16, nchunks=nch)
@@ -1044,7 +1128,8 @@ def main():
     if "host_path" in ex and not a.no_host_path:
         out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
                                                nchunks=max(8, (256 << 20) // w.chunk),
-                                               erased=[e for e in w.erased if e < w.k])
+                                               erased=[e for e in w.fixed_erased if e < w.k],
+                                               sets=w.sets)
     if "shim_path" in ex:
         out["shim_path"] = shim_path_rate(ctx)
     if "hashing" in ex:

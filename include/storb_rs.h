@@ -172,6 +172,22 @@ int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                               const uint8_t *d_parity, size_t parity_stride,
                               uint8_t *d_out, size_t out_stride,
                               void *hip_stream);
+/* Reconstruct nstripes stripes that each lost different shares -- Storb's
+ * download: per chunk the first k + 1 pieces to ARRIVE from 10 fetch threads
+ * are kept (crates/storb_validator/src/download.rs:363-451), then
+ * decode_chunk sorts them and uses the first k by index (piece.rs:368-381),
+ * so the survivor set varies from chunk to chunk. Stripe s offers nshares[s]
+ * shares, share_idx[o_s .. o_s + nshares[s]) with o_s = nshares[0] + ... +
+ * nshares[s-1]. Layout and d_out semantics as storb_rs_decode_batch_dev.
+ * One launch per missing-row count over all stripes (each workgroup reads its
+ * own stripe's pattern), not one per pattern. ENOTENOUGH names the stripe. */
+int storb_rs_decode_stripes_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                                size_t block, uint32_t nstripes,
+                                const uint32_t *share_idx, const uint32_t *nshares,
+                                const uint8_t *d_data, size_t data_stride,
+                                const uint8_t *d_parity, size_t parity_stride,
+                                uint8_t *d_out, size_t out_stride,
+                                void *hip_stream);
 /* Decode-based repair. Storb's repair today re-fetches a
  * lost piece from another replica (crates/storb_validator/src/repair.rs:
  * 44-277); with RS it can instead regenerate any share row -- data or
@@ -231,9 +247,12 @@ int storb_rs_set_kernel(storb_rs_ctx *ctx, int variant);
  * rows, k = 8..11 with >= 6, k <= 64, up to 32 rows as launches of <= 16;
  * batches >= 4 MiB)
  * gets its own bit-sliced kernel, compiled with hipRTC on a background thread
- * and cached for the process; calls made while it compiles run the table
- * kernel. STORB_RS_JIT=0 disables, =sync compiles before the first launch;
- * STORB_RS_JIT_MAX caps the number of kernels (default 256). */
+ * once the same matrix has been asked for twice, and cached; calls made
+ * before or while it compiles run the table kernel. STORB_RS_JIT=0 disables,
+ * =sync compiles before the first launch; STORB_RS_JIT_MAX caps the kernels
+ * loaded at once (default 256; past it the least recently used idle one is
+ * unloaded). storb_rs_decode_stripes_dev / decode_chunks with mixed patterns
+ * use the per-stripe table kernel and compile nothing. */
 typedef struct {
   uint64_t compiled;  /* kernels compiled and cached */
   uint64_t failed;    /* compiles that failed (those matrices use the table kernel) */
@@ -241,6 +260,8 @@ typedef struct {
   uint64_t launches;  /* launches of compiled kernels */
   uint64_t fallbacks; /* wanted a compiled kernel, ran the table kernel */
   double compile_ms;  /* total compile wall time */
+  uint64_t evicted;   /* kernels unloaded to make room (LRU, idle ones only) */
+  uint64_t loaded;    /* kernels currently cached (<= STORB_RS_JIT_MAX) */
 } storb_rs_jit_stats_t;
 int storb_rs_jit_stats(storb_rs_jit_stats_t *out);
 /* Block until no compile is pending (benchmarks and tests). */

@@ -51,7 +51,8 @@ sz = C.c_size_t
 class JitStats(C.Structure):
     """storb_rs_jit_stats_t (include/storb_rs.h)."""
     _fields_ = [("compiled", C.c_uint64), ("failed", C.c_uint64), ("pending", C.c_uint64),
-                ("launches", C.c_uint64), ("fallbacks", C.c_uint64), ("compile_ms", C.c_double)]
+                ("launches", C.c_uint64), ("fallbacks", C.c_uint64), ("compile_ms", C.c_double),
+                ("evicted", C.c_uint64), ("loaded", C.c_uint64)]
 
 
 NOTIFY_FN = C.CFUNCTYPE(None, vp)  # storb_rs_notify_fn
@@ -88,6 +89,9 @@ def _declare(L):
     L.storb_rs_decode_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
                                             C.POINTER(C.c_uint32), C.c_uint32, vp, sz, vp,
                                             sz, vp, sz, vp]
+    L.storb_rs_decode_stripes_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
+                                              C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), vp,
+                                              sz, vp, sz, vp, sz, vp]
     L.storb_rs_repair_batch_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
                                             C.POINTER(C.c_uint32), C.c_uint32,
                                             C.POINTER(C.c_uint32), C.c_uint32, vp, sz, vp,
@@ -481,6 +485,27 @@ class Context:
                                              parity_stride, d_out, out_stride, self._s(stream))
         self._check(rc, "storb_rs_decode_batch_dev")
 
+    def decode_stripes_dev(self, k: int, n: int, block: int, share_idx: Sequence[Sequence[int]],
+                           d_data: int, d_parity: int, d_out: int, data_stride: int = 0,
+                           parity_stride: int = 0, out_stride: int = 0,
+                           stream: Optional[int] = None):
+        """storb_rs_decode_stripes_dev: share_idx[s] lists the shares stripe s
+        offers (any order, >= k; its first k by index are used)."""
+        ids, cnt = encode_stripe_shares(share_idx)
+        self.decode_stripes_dev_raw(k, n, block, len(share_idx), ids, cnt, d_data, d_parity, d_out,
+                                    data_stride, parity_stride, out_stride, stream)
+
+    def decode_stripes_dev_raw(self, k: int, n: int, block: int, nstripes: int, ids, cnt,
+                               d_data: int, d_parity: int, d_out: int, data_stride: int = 0,
+                               parity_stride: int = 0, out_stride: int = 0,
+                               stream: Optional[int] = None):
+        """The same with prebuilt ctypes arrays (encode_stripe_shares), for
+        callers that replay one set of patterns (benchmarks)."""
+        rc = lib().storb_rs_decode_stripes_dev(self._h, k, n, block, nstripes, ids, cnt, d_data,
+                                               data_stride, d_parity, parity_stride, d_out,
+                                               out_stride, self._s(stream))
+        self._check(rc, "storb_rs_decode_stripes_dev")
+
     def repair_batch_dev(self, k: int, n: int, block: int, nstripes: int,
                          share_idx: Sequence[int], targets: Sequence[int], d_data: int,
                          d_parity: int, data_stride: int = 0, parity_stride: int = 0,
@@ -523,6 +548,15 @@ class Context:
 
     def sync(self):
         self._check(lib().storb_rs_sync(self._h), "storb_rs_sync")
+
+
+def encode_stripe_shares(share_idx: Sequence[Sequence[int]]):
+    """(share_idx, nshares) ctypes arrays of storb_rs_decode_stripes_dev /
+    storb_rs_decode_chunks: all stripes' share lists back to back + counts."""
+    flat = [int(i) for ids in share_idx for i in ids]
+    ids = (C.c_uint32 * max(1, len(flat)))(*flat)
+    cnt = (C.c_uint32 * max(1, len(share_idx)))(*[len(x) for x in share_idx])
+    return ids, cnt
 
 
 _tls = threading.local()

@@ -106,6 +106,21 @@ struct AsyncSlot {
   bool busy = false;
 };
 
+// A decode pattern: which share sits in each of the k slots (zfec's slot
+// arrangement of the first k by index, piece.rs:368-381), the rows of the
+// inverted survivor matrix that rebuild the missing data shares, and their
+// v_perm tables ([input][rows_bucket] PermTabs, padding rows zero) for the
+// per-stripe descriptor kernels. Cached per context (LRU by tick).
+struct Pattern {
+  std::vector<uint32_t> slot_idx;
+  std::vector<uint8_t> coef;      // e x k
+  std::vector<uint32_t> missing;  // data index (= slot) of output row r
+  std::vector<PermTab> tabs;      // k x rows_bucket(max(e, 1))
+  uint64_t tick = 0;
+};
+
+constexpr int kDescRing = 4;  // page-locked descriptor upload buffers per context
+
 struct DeviceGuard {
   int prev = -1;
   bool ok = false;
@@ -145,6 +160,14 @@ struct storb_rs_ctx {
   // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
   bool zc_batch = true;
   hipEvent_t slice_ev[storb_rs::detail::kMaxSlices] = {};  // sliced single-call pipeline
+  // Decode patterns by (k, n, slot share indices) and the page-locked ring
+  // the per-stripe descriptors are uploaded from (desc_ev[i]: that upload
+  // has been read by the device).
+  std::map<std::vector<uint32_t>, std::unique_ptr<storb_rs::detail::Pattern>> patterns;
+  uint64_t pattern_tick = 0;
+  storb_rs::detail::PinBuf desc_pin[storb_rs::detail::kDescRing];
+  hipEvent_t desc_ev[storb_rs::detail::kDescRing] = {};
+  unsigned desc_next = 0;
   // Slots of the asynchronous host calls (host_async.cpp); async_mu guards
   // the busy flags, which finish() clears without holding mu.
   std::mutex async_mu;
@@ -210,6 +233,33 @@ int repair_rows(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                 const std::vector<uint32_t> &slot_idx, const uint32_t *targets,
                 uint32_t ntargets, std::vector<uint8_t> &coef);
 HostPool &host_pool(storb_rs_ctx *ctx);
+// The decode pattern of one stripe from its offered shares (select_shares +
+// decode_rows, cached on the context); slot_pos[s] = position in share_idx[]
+// of the share in slot s.
+int get_pattern(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint32_t *share_idx,
+                uint32_t nshares, const Pattern **out, std::vector<uint32_t> &slot_pos);
+// Per-stripe descriptor launches (rs_apply_desc). Item i rebuilds the rows of
+// pattern pats[i] from the k inputs ptr[i*W .. +k) into the outputs
+// ptr[i*W + k .. + e) and, with copy, stores input j also to ptr[i*W + k +
+// kSlotR + j] (0 = not stored), W = 2k + kSlotR. Items are grouped by row
+// count, one launch per group; items with e = 0 only matter with copy.
+// Needs desc_ok(). The descriptors are uploaded stream-ordered on s.
+int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
+               const std::vector<const Pattern *> &pats, const std::vector<uint64_t> &ptr,
+               hipStream_t s);
+// Drop least recently used patterns once the cache is full (call at the
+// start of a call only: Patterns stay valid until the call returns).
+void trim_patterns(storb_rs_ctx *ctx);
+// One pattern for nstripes stripes of the device layout (storb_rs.h
+// decode_batch_dev): rebuild the missing rows into d_out, assembling the
+// present data shares too when d_out is a separate buffer.
+int decode_pattern_batch(storb_rs_ctx *ctx, uint32_t k, size_t block, uint32_t nstripes,
+                         const Pattern &p, const uint8_t *d_data, size_t data_stride,
+                         const uint8_t *d_parity, size_t parity_stride, uint8_t *d_out,
+                         size_t out_stride, hipStream_t s);
+// Whether the descriptor kernel takes this geometry (k <= kSlotK, at most
+// kSlotR rows, 16-B shares, the table-kernel variant in use).
+bool desc_ok(const storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block);
 // Wait for everything queued on the context's own streams, ignoring errors
 // (the early-error paths of the host calls, whose kernels may still be
 // reading / writing the caller's page-locked buffers).

@@ -1,0 +1,293 @@
+// decode_stripes.cpp -- decode where every stripe lost different shares.
+//
+// Storb's download keeps whichever k + 1 pieces of a chunk arrive first from
+// its 10 fetch threads (crates/storb_validator/src/download.rs:363-451), then
+// decode_chunk sorts them and takes the first k (piece.rs:368-381). So the
+// survivor set, and with it the decode matrix, varies from chunk to chunk. A
+// launch per erasure pattern would be one small launch per chunk (and, with
+// the run-time-compiled kernels, one compile per pattern). Here a batch of
+// chunks is ONE launch per missing-row count: every workgroup reads its own
+// stripe's descriptor -- the k input pointers, the rebuilt rows' pointers,
+// the assembly targets -- and its own pattern's v_perm tables
+// (rs_device.hpp rs_apply_desc; the table kernel's tile, unchanged).
+//
+// Patterns (slot arrangement, inverted rows, tables) are cached per context.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "ctx.hpp"
+
+using namespace storb_rs;
+using namespace storb_rs::detail;
+
+namespace storb_rs {
+namespace detail {
+
+constexpr size_t kPatternCap = 4096;  // cached decode patterns per context
+
+// Called at the start of a call (never inside one, so every Pattern a call
+// holds stays valid until it returns): drop the least recently used quarter
+// once the cache is full.
+void trim_patterns(storb_rs_ctx *ctx) {
+  if (ctx->patterns.size() < kPatternCap) return;
+  std::vector<uint64_t> ticks;
+  ticks.reserve(ctx->patterns.size());
+  for (auto &p : ctx->patterns) ticks.push_back(p.second->tick);
+  std::nth_element(ticks.begin(), ticks.begin() + ticks.size() / 4, ticks.end());
+  const uint64_t cut = ticks[ticks.size() / 4];
+  for (auto it = ctx->patterns.begin(); it != ctx->patterns.end();)
+    it = it->second->tick < cut ? ctx->patterns.erase(it) : std::next(it);
+}
+
+int get_pattern(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint32_t *share_idx,
+                uint32_t nshares, const Pattern **out, std::vector<uint32_t> &slot_pos) {
+  std::vector<uint32_t> slot_idx;
+  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
+  if (rc) return rc;
+  std::vector<uint32_t> key;
+  key.reserve(k + 2);
+  key.push_back(k);
+  key.push_back(n);
+  key.insert(key.end(), slot_idx.begin(), slot_idx.end());
+  auto it = ctx->patterns.find(key);
+  if (it == ctx->patterns.end()) {
+    auto p = std::make_unique<Pattern>();
+    rc = decode_rows(ctx, k, n, slot_idx, p->coef, p->missing);
+    if (rc) return rc;
+    p->slot_idx = std::move(slot_idx);
+    const uint32_t e = static_cast<uint32_t>(p->missing.size());
+    const uint32_t rb = static_cast<uint32_t>(rows_bucket(e ? e : 1));
+    if (e <= static_cast<uint32_t>(kSlotR)) {  // tables only for what rs_apply_desc takes
+      p->tabs.assign(static_cast<size_t>(k) * rb, PermTab{});
+      for (uint32_t r = 0; r < e; r++)
+        for (uint32_t j = 0; j < k; j++)
+          p->tabs[static_cast<size_t>(j) * rb + r] = perm_tab(p->coef[static_cast<size_t>(r) * k + j]);
+    }
+    it = ctx->patterns.emplace(std::move(key), std::move(p)).first;
+  }
+  it->second->tick = ++ctx->pattern_tick;
+  *out = it->second.get();
+  return STORB_RS_OK;
+}
+
+bool desc_ok(const storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block) {
+  return ctx->variant != STORB_RS_KERNEL_LDS && k >= 1 && k <= static_cast<uint32_t>(kSlotK) &&
+         std::min(k, n - k) <= static_cast<uint32_t>(kSlotR) && block % kAlign == 0;
+}
+
+int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
+               const std::vector<const Pattern *> &pats, const std::vector<uint64_t> &ptr,
+               hipStream_t s) {
+  const size_t W = 2 * static_cast<size_t>(k) + kSlotR;
+  std::vector<std::vector<uint32_t>> by_e(kSlotR + 1);
+  for (uint32_t i = 0; i < pats.size(); i++) {
+    const size_t e = pats[i]->missing.size();
+    if (e > static_cast<size_t>(kSlotR)) return fail(ctx, STORB_RS_EINVAL, "apply_desc: > 16 rows");
+    if (e || copy) by_e[e].push_back(i);
+  }
+  struct Group {
+    uint32_t e, rb, rec_q, nitems;
+    size_t tab_off, rec_off;
+    std::vector<const Pattern *> distinct;
+  };
+  std::vector<Group> groups;
+  size_t total = 0;
+  std::vector<uint32_t> local(pats.size());
+  for (uint32_t e = 0; e <= static_cast<uint32_t>(kSlotR); e++) {
+    if (by_e[e].empty()) continue;
+    Group g{};
+    g.e = e;
+    g.rb = static_cast<uint32_t>(rows_bucket(e ? e : 1));
+    g.rec_q = 1 + k + e + (copy ? k : 0);
+    g.nitems = static_cast<uint32_t>(by_e[e].size());
+    std::unordered_map<const Pattern *, uint32_t> seen;
+    for (uint32_t i : by_e[e]) {
+      auto f = seen.emplace(pats[i], static_cast<uint32_t>(g.distinct.size()));
+      if (f.second) g.distinct.push_back(pats[i]);
+      local[i] = f.first->second;
+    }
+    g.tab_off = total;
+    total = round_up(total + g.distinct.size() * k * g.rb * sizeof(PermTab), 256);
+    g.rec_off = total;
+    total = round_up(total + static_cast<size_t>(g.nitems) * g.rec_q * 8, 256);
+    groups.push_back(std::move(g));
+  }
+  if (groups.empty()) return STORB_RS_OK;
+  // Page-locked upload slot: reusable once its previous upload was read.
+  const unsigned slot = ctx->desc_next++ % kDescRing;
+  if (ctx->desc_ev[slot]) HIP_TRY(ctx, hipEventSynchronize(ctx->desc_ev[slot]));
+  else HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_ev[slot], hipEventDisableTiming));
+  HIP_TRY(ctx, ctx->desc_pin[slot].ensure(total));
+  uint8_t *h = ctx->desc_pin[slot].p;
+  for (const Group &g : groups) {
+    PermTab *t = reinterpret_cast<PermTab *>(h + g.tab_off);
+    for (size_t d = 0; d < g.distinct.size(); d++)
+      std::memcpy(t + d * k * g.rb, g.distinct[d]->tabs.data(),
+                  static_cast<size_t>(k) * g.rb * sizeof(PermTab));
+    uint64_t *rec = reinterpret_cast<uint64_t *>(h + g.rec_off);
+    for (uint32_t i : by_e[g.e]) {
+      const uint64_t *src = &ptr[i * W];
+      rec[0] = local[i];
+      std::memcpy(rec + 1, src, static_cast<size_t>(k) * 8);
+      std::memcpy(rec + 1 + k, src + k, static_cast<size_t>(g.e) * 8);
+      if (copy) std::memcpy(rec + 1 + k + g.e, src + k + kSlotR, static_cast<size_t>(k) * 8);
+      rec += g.rec_q;
+    }
+  }
+  uint8_t *dev = nullptr;
+  HIP_TRY(ctx, hipMallocAsync(reinterpret_cast<void **>(&dev), total, s));
+  hipError_t e = hipMemcpyAsync(dev, h, total, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(ctx->desc_ev[slot], s);
+  for (size_t gi = 0; e == hipSuccess && gi < groups.size(); gi++) {
+    const Group &g = groups[gi];
+    DescArgs a{};
+    a.desc = reinterpret_cast<const uint64_t *>(dev + g.rec_off);
+    a.ptab = reinterpret_cast<const PermTab *>(dev + g.tab_off);
+    a.block = block;
+    a.k = k;
+    a.r = g.e;
+    a.tab_rows = g.rb;
+    a.nitems = g.nitems;
+    a.copy = copy ? 1u : 0u;
+    a.rec_qwords = g.rec_q;
+    e = launch_apply_desc(a, s);
+  }
+  const hipError_t ef = hipFreeAsync(dev, s);  // ordered after the launches
+  if (e != hipSuccess) return hip_fail(ctx, e, "apply_desc");
+  if (ef != hipSuccess) return hip_fail(ctx, ef, "hipFreeAsync(descriptors)");
+  return STORB_RS_OK;
+}
+
+// One pattern for nstripes stripes of the device layout (storb_rs.h): the
+// uniform batch decode. Compiled bit-sliced kernels where the policy wants
+// them (apply); fused assembly when d_out is a separate buffer.
+int decode_pattern_batch(storb_rs_ctx *ctx, uint32_t k, size_t block, uint32_t nstripes,
+                         const Pattern &p, const uint8_t *d_data, size_t data_stride,
+                         const uint8_t *d_parity, size_t parity_stride, uint8_t *d_out,
+                         size_t out_stride, hipStream_t s) {
+  std::vector<const uint8_t *> in(k);
+  std::vector<size_t> ins(k);
+  for (uint32_t c = 0; c < k; c++) {
+    const uint32_t id = p.slot_idx[c];
+    if (id < k) {
+      if (!d_data) return fail(ctx, STORB_RS_EINVAL, "survivor in null data region");
+      in[c] = d_data + static_cast<size_t>(id) * block;
+      ins[c] = data_stride;
+    } else {
+      if (!d_parity) return fail(ctx, STORB_RS_EINVAL, "survivor in null parity region");
+      in[c] = d_parity + static_cast<size_t>(id - k) * block;
+      ins[c] = parity_stride;
+    }
+  }
+  const size_t e = p.missing.size();
+  std::vector<uint8_t *> out(e);
+  std::vector<size_t> outs(e, out_stride);
+  for (size_t r = 0; r < e; r++) out[r] = d_out + static_cast<size_t>(p.missing[r]) * block;
+  // Surviving data shares: in place when d_out aliases d_data; else stored
+  // to their slots of d_out by the decode kernel itself as it reads them
+  // (fused assembly), or, where no such kernel applies, copied first (apply).
+  const bool assemble = d_out != d_data || out_stride != data_stride;
+  std::vector<uint8_t *> copy(k, nullptr);
+  std::vector<size_t> copys(k, out_stride);
+  if (assemble)
+    for (uint32_t c = 0; c < k; c++)
+      if (p.slot_idx[c] < k) copy[c] = d_out + static_cast<size_t>(c) * block;
+  return apply(ctx, k, static_cast<uint32_t>(e), p.coef.data(), in.data(), ins.data(), out.data(),
+               outs.data(), block, nstripes, s, assemble ? copy.data() : nullptr,
+               assemble ? copys.data() : nullptr);
+}
+
+}  // namespace detail
+}  // namespace storb_rs
+
+extern "C" {
+
+int storb_rs_decode_stripes_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                                uint32_t nstripes, const uint32_t *share_idx,
+                                const uint32_t *nshares, const uint8_t *d_data,
+                                size_t data_stride, const uint8_t *d_parity,
+                                size_t parity_stride, uint8_t *d_out, size_t out_stride,
+                                void *hip_stream) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (nstripes && (!share_idx || !nshares || !d_out))
+    return fail(ctx, STORB_RS_EINVAL, "null argument");
+  if (data_stride == 0) data_stride = static_cast<size_t>(k) * block;
+  if (parity_stride == 0) parity_stride = static_cast<size_t>(n - k) * block;
+  if (out_stride == 0) out_stride = static_cast<size_t>(k) * block;
+  trim_patterns(ctx);
+  std::vector<const Pattern *> pats(nstripes);
+  std::vector<uint32_t> slot_pos;
+  size_t off = 0;
+  bool uniform = true;
+  for (uint32_t st = 0; st < nstripes; st++) {
+    const int rc = get_pattern(ctx, k, n, share_idx + off, nshares[st], &pats[st], slot_pos);
+    if (rc) {
+      ctx->last_error += " (stripe " + std::to_string(st) + ")";
+      return rc;
+    }
+    off += nshares[st];
+    uniform = uniform && pats[st] == pats[0];
+  }
+  if (block == 0 || nstripes == 0) return STORB_RS_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = pick_stream(ctx, hip_stream);
+  const bool assemble = d_out != d_data || out_stride != data_stride;
+  if (uniform)  // one pattern: the uniform path (compiled kernels, where wanted)
+    return decode_pattern_batch(ctx, k, block, nstripes, *pats[0], d_data, data_stride, d_parity,
+                                parity_stride, d_out, out_stride, s);
+  auto al = [](const void *p, size_t st) { return ((reinterpret_cast<uintptr_t>(p) | st) % kAlign) == 0; };
+  bool need_data = false, need_par = false;
+  for (const Pattern *p : pats)
+    for (uint32_t c = 0; c < k; c++) (p->slot_idx[c] < k ? need_data : need_par) = true;
+  if (need_data && !d_data) return fail(ctx, STORB_RS_EINVAL, "survivor in null data region");
+  if (need_par && !d_parity) return fail(ctx, STORB_RS_EINVAL, "survivor in null parity region");
+  if (!desc_ok(ctx, k, n, block) || !al(d_data, data_stride) || !al(d_parity, parity_stride) ||
+      !al(d_out, out_stride)) {
+    // Geometries the descriptor kernel does not take: one launch per run of
+    // consecutive stripes with the same pattern.
+    for (uint32_t a = 0; a < nstripes;) {
+      uint32_t b = a + 1;
+      while (b < nstripes && pats[b] == pats[a]) b++;
+      const int rc = decode_pattern_batch(
+          ctx, k, block, b - a, *pats[a], d_data ? d_data + a * data_stride : nullptr, data_stride,
+          d_parity ? d_parity + a * parity_stride : nullptr, parity_stride,
+          d_out + a * out_stride, out_stride, s);
+      if (rc) return rc;
+      a = b;
+    }
+    return STORB_RS_OK;
+  }
+  // Assembly into a separate buffer: stored by the kernel from its own loads
+  // for k <= kCopyMaxK; wider codes copy all data slots first (one 2-D copy)
+  // and rebuild the missing rows over them.
+  const bool fused = assemble && k <= kCopyMaxK;
+  if (assemble && !fused)
+    HIP_TRY(ctx, hipMemcpy2DAsync(d_out, out_stride, d_data, data_stride,
+                                  static_cast<size_t>(k) * block, nstripes,
+                                  hipMemcpyDeviceToDevice, s));
+  const size_t W = 2 * static_cast<size_t>(k) + kSlotR;
+  std::vector<uint64_t> ptr(static_cast<size_t>(nstripes) * W, 0);
+  for (uint32_t st = 0; st < nstripes; st++) {
+    const Pattern &p = *pats[st];
+    uint64_t *q = &ptr[st * W];
+    for (uint32_t c = 0; c < k; c++) {
+      const uint32_t id = p.slot_idx[c];
+      q[c] = id < k ? reinterpret_cast<uint64_t>(d_data + st * data_stride + id * block)
+                    : reinterpret_cast<uint64_t>(d_parity + st * parity_stride + (id - k) * block);
+      if (fused && id < k)
+        q[k + kSlotR + c] = reinterpret_cast<uint64_t>(d_out + st * out_stride + id * block);
+    }
+    for (size_t r = 0; r < p.missing.size(); r++)
+      q[k + r] = reinterpret_cast<uint64_t>(d_out + st * out_stride + p.missing[r] * block);
+  }
+  return apply_desc(ctx, k, block, fused, pats, ptr, s);
+}
+
+}  // extern "C"

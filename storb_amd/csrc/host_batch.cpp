@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -172,12 +173,109 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
 
 // Pipelined batch decode (the download path, download.rs:453-465, one
 // chunk after another today). Every chunk selects its first k shares by
-// index (decode_chunk, piece.rs:368-381). Chunks whose k data shares are all
-// present are pure host copies; the rest are grouped by erasure pattern, so
-// each batch is one launch of one decode matrix, and stream through the same
-// double-buffered pinned pipeline as encode: pack the k survivors into
-// pinned staging (present data shares also go straight to `out`), H2D,
-// rebuild only the missing rows, D2H them, unpack into `out`.
+// index (decode_chunk, piece.rs:368-381) -- which shares those are differs
+// from chunk to chunk, since Storb keeps the first k + 1 pieces to arrive
+// (download.rs:363-451). Chunks whose k data shares are all present are pure
+// host copies. The rest go, in order and whatever their erasure patterns, to
+// per-stripe descriptor launches (decode_stripes.cpp): one launch per
+// missing-row count per batch, each workgroup with its own chunk's pointers
+// and matrix.
+//  * Zero-copy: page-locked, aligned shares and output (storb_rs_host_alloc /
+//    _register): the kernel reads the k survivors over PCIe where they lie
+//    and writes only the rebuilt rows into `out`, while the host pool copies
+//    the present data shares into `out` (disjoint rows).
+//  * Staged: double-buffered pinned batches -- pack the k survivors into
+//    pinned staging (present data shares also go straight to `out`), H2D,
+//    rebuild the missing rows, D2H them, unpack into `out`.
+// Geometries the descriptor kernel does not take (k > 32, > 16 rebuilt rows,
+// the LDS comparison variant) run the staged pipeline with one launch per
+// pattern group (decode_chunks_grouped).
+static int decode_chunks_grouped(storb_rs_ctx *ctx, uint32_t k, size_t block, size_t outlen,
+                                 const std::vector<uint32_t> &rest,
+                                 const std::vector<const Pattern *> &pats,
+                                 const std::vector<const uint8_t *> &slot_ptr, uint8_t *out,
+                                 size_t out_stride) {
+  HostPool &pool = host_pool(ctx);
+  auto put_row = [&](uint32_t c, uint32_t row, const uint8_t *src) {
+    const size_t o = static_cast<size_t>(row) * block;
+    if (o < outlen)
+      std::memcpy(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
+  };
+  std::map<const Pattern *, std::vector<uint32_t>> groups;
+  for (uint32_t c : rest) groups[pats[c]].push_back(c);
+  struct Item {
+    const Pattern *pat;
+    const uint32_t *chunks;
+    uint32_t cn;
+  };
+  const size_t S = round_up(block, kAlign);
+  const size_t per = static_cast<size_t>(k) * S;
+  uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
+  std::vector<Item> items;
+  uint32_t emax = 0;
+  for (auto &g : groups) {
+    emax = std::max<uint32_t>(emax, static_cast<uint32_t>(g.first->missing.size()));
+    for (size_t i = 0; i < g.second.size(); i += batch)
+      items.push_back(Item{g.first, g.second.data() + i,
+                           static_cast<uint32_t>(std::min<size_t>(batch, g.second.size() - i))});
+  }
+  batch = 0;
+  for (auto &it : items) batch = std::max(batch, it.cn);
+  for (int b = 0; b < 2; b++) {
+    HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
+    HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(emax) * S * batch));
+    HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(k + emax) * S * batch));
+  }
+  auto unpack = [&](size_t ii) {
+    const Item &it = items[ii];
+    const uint8_t *src = ctx->pipe_out[ii & 1].p;
+    const uint32_t e = static_cast<uint32_t>(it.pat->missing.size());
+    pool.run(static_cast<int>(it.cn), [&](int c) {
+      for (uint32_t r = 0; r < e; r++)
+        put_row(it.chunks[c], it.pat->missing[r], src + (static_cast<size_t>(c) * e + r) * S);
+    });
+  };
+  for (size_t ii = 0; ii < items.size(); ii++) {
+    const int b = ii & 1;
+    hipStream_t s = ctx->pipe[b];
+    if (ii >= 2) {  // pinned pair b is free once item ii-2 has landed
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      unpack(ii - 2);
+    }
+    const Item &it = items[ii];
+    const uint32_t e = static_cast<uint32_t>(it.pat->missing.size());
+    uint8_t *hin = ctx->pipe_in[b].p;
+    pool.run(static_cast<int>(it.cn), [&](int c) {
+      const uint32_t ch = it.chunks[c];
+      for (uint32_t sl = 0; sl < k; sl++) {
+        const uint8_t *src = slot_ptr[static_cast<size_t>(ch) * k + sl];
+        uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(sl) * S;
+        std::memcpy(dst, src, block);
+        if (S > block) std::memset(dst + block, 0, S - block);
+        if (it.pat->slot_idx[sl] == sl) put_row(ch, sl, src);  // present data share
+      }
+    });
+    uint8_t *dd = ctx->pipe_dev[b].p;
+    uint8_t *dm = dd + per * it.cn;
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * it.cn, hipMemcpyHostToDevice, s));
+    std::vector<const uint8_t *> in(k);
+    std::vector<uint8_t *> o(e);
+    std::vector<size_t> ins(k, per), outs(e, static_cast<size_t>(e) * S);
+    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
+    for (uint32_t r = 0; r < e; r++) o[r] = dm + static_cast<size_t>(r) * S;
+    const int rc = apply(ctx, k, e, it.pat->coef.data(), in.data(), ins.data(), o.data(),
+                         outs.data(), S, it.cn, s);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(e) * S * it.cn,
+                                hipMemcpyDeviceToHost, s));
+  }
+  for (size_t ii = items.size() >= 2 ? items.size() - 2 : 0; ii < items.size(); ii++) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[ii & 1]));
+    unpack(ii);
+  }
+  return STORB_RS_OK;
+}
+
 static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
                                 size_t padlen, uint32_t nchunks, const uint8_t *const *shares,
                                 const uint32_t *share_idx, const uint32_t *nshares,
@@ -190,34 +288,28 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   const size_t outlen = static_cast<size_t>(k) * block - padlen;
   if (out_stride == 0) out_stride = outlen;
   if (out_stride < outlen) return fail(ctx, STORB_RS_EINVAL, "decode_chunks: out_stride < chunk");
-  // per chunk: its k slot shares (pointers) and erasure pattern
+  trim_patterns(ctx);
+  // per chunk: its pattern and its k slot shares (pointers)
+  std::vector<const Pattern *> pats(nchunks);
   std::vector<const uint8_t *> slot_ptr(static_cast<size_t>(nchunks) * k);
-  std::vector<uint8_t> slot_is_data(static_cast<size_t>(nchunks) * k);  // slot s holds share s
-  std::map<std::vector<uint32_t>, std::vector<uint32_t>> groups;
-  std::vector<uint32_t> plain;
+  std::vector<uint32_t> plain, rest, slot_pos;
   size_t off = 0;
   for (uint32_t c = 0; c < nchunks; c++) {
-    std::vector<uint32_t> slot_idx, slot_pos;
-    const int rc = select_shares(ctx, k, n, share_idx + off, nshares[c], slot_idx, slot_pos);
+    const int rc = get_pattern(ctx, k, n, share_idx + off, nshares[c], &pats[c], slot_pos);
     if (rc) {
       ctx->last_error += " (chunk " + std::to_string(c) + ")";
       return rc;
     }
     for (uint32_t s = 0; s < k; s++) {
       slot_ptr[static_cast<size_t>(c) * k + s] = shares[off + slot_pos[s]];
-      slot_is_data[static_cast<size_t>(c) * k + s] = slot_idx[s] == s;
       if (!slot_ptr[static_cast<size_t>(c) * k + s])
         return fail(ctx, STORB_RS_EINVAL, "decode_chunks: null share");
     }
     off += nshares[c];
-    bool all_data = true;
-    for (uint32_t s = 0; s < k; s++) all_data &= slot_idx[s] == s;
-    if (all_data)
-      plain.push_back(c);
-    else
-      groups[slot_idx].push_back(c);
+    (pats[c]->missing.empty() ? plain : rest).push_back(c);
   }
   HostPool &pool = host_pool(ctx);
+  auto sp = [&](uint32_t c, uint32_t sl) { return slot_ptr[static_cast<size_t>(c) * k + sl]; };
   auto put_row = [&](uint32_t c, uint32_t row, const uint8_t *src) {
     const size_t o = static_cast<size_t>(row) * block;
     if (o < outlen)
@@ -225,211 +317,132 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   };
   if (!plain.empty())  // all data shares present: concatenation (zfec does the same)
     pool.run(static_cast<int>(plain.size()), [&](int i) {
-      for (uint32_t s = 0; s < k; s++)
-        put_row(plain[i], s, slot_ptr[static_cast<size_t>(plain[i]) * k + s]);
+      for (uint32_t s = 0; s < k; s++) put_row(plain[i], s, sp(plain[i], s));
     });
-  if (groups.empty()) return STORB_RS_OK;
-
-  // Zero-copy groups: page-locked caller shares AND output (storb_rs_host_alloc
-  // / _register), no padding, 16-B aligned. The decode kernel reads the k
-  // survivors over PCIe where they lie and writes the rebuilt rows and the
-  // surviving data shares (fused assembly) straight into `out`: no host copy
-  // at all, where the staged path below copies 2 k B per chunk on the host
-  // (survivors into staging, present shares into out) and is bound by it.
-  // Chunks of a group whose share pointers advance by one constant per slot
-  // (an arena of equal chunks) share a launch; others get one launch each.
-  const bool zc_out = ctx->zc_batch && padlen == 0 && block % kAlign == 0 &&
-                      out_stride % kAlign == 0 && reinterpret_cast<uintptr_t>(out) % kAlign == 0 &&
-                      range_pinned(out, static_cast<size_t>(nchunks - 1) * out_stride + outlen);
-  auto share_zc = [&](uint32_t c) {
-    for (uint32_t sl = 0; sl < k; sl++) {
-      const uint8_t *p = slot_ptr[static_cast<size_t>(c) * k + sl];
-      if (reinterpret_cast<uintptr_t>(p) % kAlign || !range_pinned(p, block)) return false;
-    }
-    return true;
-  };
-  // Device address of a page-locked pointer: one hipHostGetDevicePointer per
-  // registered range (a range maps linearly), not one per share.
-  std::map<const uint8_t *, uint8_t *> dev_base;
-  auto dev_ptr = [&](const uint8_t *p, size_t len, uint8_t **d) -> hipError_t {
-    const uint8_t *b = pinned_base(p, len);
-    if (!b) return hipErrorInvalidValue;
-    auto f = dev_base.find(b);
-    if (f == dev_base.end()) {
-      uint8_t *db = nullptr;
-      const hipError_t e = host_dev_ptr(const_cast<uint8_t *>(b), &db);
-      if (e != hipSuccess) return e;
-      f = dev_base.emplace(b, db).first;
-    }
-    *d = f->second + (p - b);
-    return hipSuccess;
-  };
-  // Who assembles the surviving data shares into `out` on the zero-copy path:
-  // the host copy pool while the kernels run (default: PCIe then carries only
-  // the k survivors in and the e rebuilt rows out), or the kernel itself
-  // (STORB_RS_ZC_ASSEMBLY=kernel: fused assembly, k rows out over PCIe).
-  static const bool host_assembly = [] {
-    const char *e = std::getenv("STORB_RS_ZC_ASSEMBLY");
-    return !(e && std::strcmp(e, "kernel") == 0);
-  }();
-  std::vector<uint32_t> zc_chunks;  // chunks whose present data shares the host copies
+  if (rest.empty()) return STORB_RS_OK;
   DeviceGuard dg(ctx->device);
-  uint32_t zc_launches = 0;
-  for (auto it = groups.begin(); zc_out && it != groups.end();) {
-    const std::vector<uint32_t> &slots = it->first, &cs = it->second;
-    bool ok = true;
-    for (uint32_t c : cs) ok = ok && share_zc(c);
-    if (!ok) {
-      ++it;
-      continue;
-    }
-    std::vector<uint8_t> coef;
-    std::vector<uint32_t> missing;
-    int rc = decode_rows(ctx, k, n, slots, coef, missing);
-    if (rc) return rc;
-    const uint32_t e = static_cast<uint32_t>(missing.size());
-    auto sp = [&](uint32_t c, uint32_t sl) { return slot_ptr[static_cast<size_t>(c) * k + sl]; };
-    // chunk i + 1 continues the run of chunk i with steps (dc, dp[])
-    auto step_ok = [&](size_t i, uint32_t dc, const std::vector<uintptr_t> &dp) {
-      if (cs[i + 1] - cs[i] != dc) return false;
-      for (uint32_t sl = 0; sl < k; sl++)
-        if (reinterpret_cast<uintptr_t>(sp(cs[i + 1], sl)) - reinterpret_cast<uintptr_t>(sp(cs[i], sl)) != dp[sl])
-          return false;
-      return true;
-    };
-    for (size_t i = 0; i < cs.size();) {
-      size_t j = i + 1;
-      uint32_t dc = 0;
-      std::vector<uintptr_t> dp(k, block);
-      if (j < cs.size()) {
-        dc = cs[j] - cs[i];
-        bool fwd = true;  // strides are unsigned and kept 16-B aligned
-        for (uint32_t sl = 0; sl < k; sl++) {
-          dp[sl] = reinterpret_cast<uintptr_t>(sp(cs[j], sl)) - reinterpret_cast<uintptr_t>(sp(cs[i], sl));
-          fwd = fwd && reinterpret_cast<uintptr_t>(sp(cs[j], sl)) > reinterpret_cast<uintptr_t>(sp(cs[i], sl)) &&
-                dp[sl] % kAlign == 0;
-        }
-        if (fwd)
-          while (j < cs.size() && step_ok(j - 1, dc, dp)) j++;
-        else
-          dp.assign(k, block);
-      }
-      const uint32_t cn = static_cast<uint32_t>(j - i);
-      uint8_t *obase = out + static_cast<size_t>(cs[i]) * out_stride;
-      // (one chunk: any pitch >= a share does; copy-first assembly needs one)
-      const size_t ostr = cn > 1 ? static_cast<size_t>(dc) * out_stride : outlen;
-      std::vector<const uint8_t *> in(k);
-      std::vector<size_t> ins(k);
-      std::vector<uint8_t *> cp(k, nullptr), o(e);
-      std::vector<size_t> cps(k, ostr), outs(e, ostr);
-      for (uint32_t sl = 0; sl < k; sl++) {
-        uint8_t *d = nullptr;
-        HIP_TRY(ctx, dev_ptr(sp(cs[i], sl), block, &d));
-        in[sl] = d;
-        ins[sl] = cn > 1 ? dp[sl] : block;
-        if (slots[sl] == sl && !host_assembly)  // present data share: assembled by the kernel
-          HIP_TRY(ctx, dev_ptr(obase + static_cast<size_t>(sl) * block, block, &cp[sl]));
-      }
-      for (uint32_t r = 0; r < e; r++)
-        HIP_TRY(ctx, dev_ptr(obase + static_cast<size_t>(missing[r]) * block, block, &o[r]));
-      rc = apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), block, cn,
-                 ctx->pipe[zc_launches++ & 1], host_assembly ? nullptr : cp.data(), cps.data());
-      if (rc) return rc;
-      i = j;
-    }
-    if (host_assembly) zc_chunks.insert(zc_chunks.end(), cs.begin(), cs.end());
-    it = groups.erase(it);
-  }
-  if (!zc_chunks.empty()) {  // overlaps the kernels (disjoint rows of out)
-    std::vector<std::pair<uint32_t, uint32_t>> rows;  // (chunk, present data slot)
-    for (uint32_t c : zc_chunks)
-      for (uint32_t sl = 0; sl < k; sl++)
-        if (slot_is_data[static_cast<size_t>(c) * k + sl]) rows.emplace_back(c, sl);
-    pool.run(static_cast<int>(rows.size()), [&](int i) {
-      put_row(rows[i].first, rows[i].second,
-              slot_ptr[static_cast<size_t>(rows[i].first) * k + rows[i].second]);
-    });
-  }
-  if (zc_launches)
-    for (int b = 0; b < 2; b++) HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[b]));
-  if (groups.empty()) return STORB_RS_OK;
-
-  struct Item {
-    const std::vector<uint32_t> *slots;
-    const uint32_t *chunks;
-    uint32_t cn;
-    std::vector<uint8_t> coef;
-    std::vector<uint32_t> missing;
-  };
   const size_t S = round_up(block, kAlign);
-  const size_t per = static_cast<size_t>(k) * S;
-  uint32_t batch = static_cast<uint32_t>(std::max<size_t>(1, (64ull << 20) / per));
-  std::vector<Item> items;
-  uint32_t emax = 0;
-  for (auto &g : groups) {
-    std::vector<uint8_t> coef;
-    std::vector<uint32_t> missing;
-    const int rc = decode_rows(ctx, k, n, g.first, coef, missing);
-    if (rc) return rc;
-    emax = std::max<uint32_t>(emax, static_cast<uint32_t>(missing.size()));
-    for (size_t i = 0; i < g.second.size(); i += batch)
-      items.push_back(Item{&g.first, g.second.data() + i,
-                           static_cast<uint32_t>(std::min<size_t>(batch, g.second.size() - i)),
-                           coef, missing});
+  if (!desc_ok(ctx, k, n, S))
+    return decode_chunks_grouped(ctx, k, block, outlen, rest, pats, slot_ptr, out, out_stride);
+  const size_t W = 2 * static_cast<size_t>(k) + kSlotR;
+
+  // Zero-copy chunks: page-locked caller shares AND output, no padding.
+  const bool zc_out = ctx->zc_batch && padlen == 0 && block % kAlign == 0 &&
+                      out_stride % kAlign == 0 &&
+                      reinterpret_cast<uintptr_t>(out) % kAlign == 0 &&
+                      range_pinned(out, static_cast<size_t>(nchunks - 1) * out_stride + outlen);
+  std::vector<uint32_t> zc, staged;
+  for (uint32_t c : rest) {
+    bool ok = zc_out;
+    for (uint32_t sl = 0; ok && sl < k; sl++)
+      ok = reinterpret_cast<uintptr_t>(sp(c, sl)) % kAlign == 0 && range_pinned(sp(c, sl), block);
+    (ok ? zc : staged).push_back(c);
   }
-  batch = 0;
-  for (auto &it : items) batch = std::max(batch, it.cn);
+  if (!zc.empty()) {
+    // Device address of a page-locked pointer: one hipHostGetDevicePointer
+    // per registered range (a range maps linearly), not one per share.
+    std::map<const uint8_t *, uint8_t *> dev_base;
+    auto dev_ptr = [&](const uint8_t *p, size_t len, uint64_t *d) -> hipError_t {
+      const uint8_t *b = pinned_base(p, len);
+      if (!b) return hipErrorInvalidValue;
+      auto f = dev_base.find(b);
+      if (f == dev_base.end()) {
+        uint8_t *db = nullptr;
+        const hipError_t e = host_dev_ptr(const_cast<uint8_t *>(b), &db);
+        if (e != hipSuccess) return e;
+        f = dev_base.emplace(b, db).first;
+      }
+      *d = reinterpret_cast<uint64_t>(f->second + (p - b));
+      return hipSuccess;
+    };
+    std::vector<const Pattern *> zp(zc.size());
+    std::vector<uint64_t> ptr(zc.size() * W, 0);
+    for (size_t i = 0; i < zc.size(); i++) {
+      const uint32_t c = zc[i];
+      zp[i] = pats[c];
+      for (uint32_t sl = 0; sl < k; sl++) HIP_TRY(ctx, dev_ptr(sp(c, sl), block, &ptr[i * W + sl]));
+      uint8_t *ob = out + static_cast<size_t>(c) * out_stride;
+      for (size_t r = 0; r < pats[c]->missing.size(); r++)
+        HIP_TRY(ctx, dev_ptr(ob + pats[c]->missing[r] * block, block, &ptr[i * W + k + r]));
+    }
+    int rc = apply_desc(ctx, k, block, false, zp, ptr, ctx->pipe[0]);
+    if (rc) return rc;
+    std::vector<std::pair<uint32_t, uint32_t>> rows;  // (chunk, present data slot)
+    for (uint32_t c : zc)
+      for (uint32_t sl = 0; sl < k; sl++)
+        if (pats[c]->slot_idx[sl] == sl) rows.emplace_back(c, sl);
+    pool.run(static_cast<int>(rows.size()), [&](int i) {  // overlaps the kernels
+      put_row(rows[i].first, rows[i].second, sp(rows[i].first, rows[i].second));
+    });
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[0]));
+  }
+  if (staged.empty()) return STORB_RS_OK;
+
+  // Staged: batches of chunks in order, ~64 MiB of survivors each.
+  const size_t per = static_cast<size_t>(k) * S;
+  const uint32_t batch = static_cast<uint32_t>(
+      std::min<size_t>(staged.size(), std::max<size_t>(1, (64ull << 20) / per)));
+  uint32_t emax = 0;
+  for (uint32_t c : staged) emax = std::max<uint32_t>(emax, static_cast<uint32_t>(pats[c]->missing.size()));
   for (int b = 0; b < 2; b++) {
     HIP_TRY(ctx, ctx->pipe_in[b].ensure(per * batch));
     HIP_TRY(ctx, ctx->pipe_out[b].ensure(static_cast<size_t>(emax) * S * batch));
     HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(k + emax) * S * batch));
   }
-  auto unpack = [&](size_t ii) {
-    const Item &it = items[ii];
-    const uint8_t *src = ctx->pipe_out[ii & 1].p;
-    const uint32_t e = static_cast<uint32_t>(it.missing.size());
-    pool.run(static_cast<int>(it.cn), [&](int c) {
-      for (uint32_t r = 0; r < e; r++)
-        put_row(it.chunks[c], it.missing[r], src + (static_cast<size_t>(c) * e + r) * S);
+  const uint32_t nb = static_cast<uint32_t>((staged.size() + batch - 1) / batch);
+  // rebuilt row r of the c-th chunk of a batch: pitch emax rows per chunk
+  auto unpack = [&](uint32_t bi) {
+    const uint8_t *src = ctx->pipe_out[bi & 1].p;
+    const uint32_t c0 = bi * batch, cn = std::min<uint32_t>(batch, static_cast<uint32_t>(staged.size()) - c0);
+    pool.run(static_cast<int>(cn), [&](int c) {
+      const uint32_t ch = staged[c0 + c];
+      const Pattern &p = *pats[ch];
+      for (size_t r = 0; r < p.missing.size(); r++)
+        put_row(ch, p.missing[r], src + (static_cast<size_t>(c) * emax + r) * S);
     });
   };
-  for (size_t ii = 0; ii < items.size(); ii++) {
-    const int b = ii & 1;
+  std::vector<const Pattern *> bp;
+  std::vector<uint64_t> ptr;
+  for (uint32_t bi = 0; bi < nb; bi++) {
+    const int b = bi & 1;
     hipStream_t s = ctx->pipe[b];
-    if (ii >= 2) {  // pinned pair b is free once item ii-2 has landed
+    if (bi >= 2) {  // pinned pair b is free once batch bi-2 has landed
       HIP_TRY(ctx, hipStreamSynchronize(s));
-      unpack(ii - 2);
+      unpack(bi - 2);
     }
-    const Item &it = items[ii];
-    const uint32_t e = static_cast<uint32_t>(it.missing.size());
+    const uint32_t c0 = bi * batch, cn = std::min<uint32_t>(batch, static_cast<uint32_t>(staged.size()) - c0);
     uint8_t *hin = ctx->pipe_in[b].p;
-    pool.run(static_cast<int>(it.cn), [&](int c) {
-      const uint32_t ch = it.chunks[c];
+    pool.run(static_cast<int>(cn), [&](int c) {
+      const uint32_t ch = staged[c0 + c];
       for (uint32_t sl = 0; sl < k; sl++) {
-        const uint8_t *src = slot_ptr[static_cast<size_t>(ch) * k + sl];
         uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(sl) * S;
-        std::memcpy(dst, src, block);
+        std::memcpy(dst, sp(ch, sl), block);
         if (S > block) std::memset(dst + block, 0, S - block);
-        if ((*it.slots)[sl] == sl) put_row(ch, sl, src);  // present data share
+        if (pats[ch]->slot_idx[sl] == sl) put_row(ch, sl, sp(ch, sl));  // present data share
       }
     });
     uint8_t *dd = ctx->pipe_dev[b].p;
-    uint8_t *dm = dd + per * it.cn;
-    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * it.cn, hipMemcpyHostToDevice, s));
-    std::vector<const uint8_t *> in(k);
-    std::vector<uint8_t *> o(e);
-    std::vector<size_t> ins(k, per), outs(e, static_cast<size_t>(e) * S);
-    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
-    for (uint32_t r = 0; r < e; r++) o[r] = dm + static_cast<size_t>(r) * S;
-    const int rc = apply(ctx, k, e, it.coef.data(), in.data(), ins.data(), o.data(), outs.data(),
-                         S, it.cn, s);
+    uint8_t *dm = dd + per * batch;
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
+    bp.assign(cn, nullptr);
+    ptr.assign(static_cast<size_t>(cn) * W, 0);
+    for (uint32_t c = 0; c < cn; c++) {
+      const Pattern &p = *pats[staged[c0 + c]];
+      bp[c] = &p;
+      for (uint32_t sl = 0; sl < k; sl++)
+        ptr[c * W + sl] = reinterpret_cast<uint64_t>(dd + static_cast<size_t>(c) * per + sl * S);
+      for (size_t r = 0; r < p.missing.size(); r++)
+        ptr[c * W + k + r] = reinterpret_cast<uint64_t>(dm + (static_cast<size_t>(c) * emax + r) * S);
+    }
+    // staged shares are S-pitched: the kernel works on S-byte rows
+    const int rc = apply_desc(ctx, k, S, false, bp, ptr, s);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(e) * S * it.cn,
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(emax) * S * cn,
                                 hipMemcpyDeviceToHost, s));
   }
-  for (size_t ii = items.size() >= 2 ? items.size() - 2 : 0; ii < items.size(); ii++) {
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[ii & 1]));
-    unpack(ii);
+  for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[bi & 1]));
+    unpack(bi);
   }
   return STORB_RS_OK;
 }

@@ -104,28 +104,28 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   std::vector<uint8_t *> out(p);
   std::vector<size_t> ins(k, static_cast<size_t>(k) * S), outs(p, static_cast<size_t>(p) * S);
   // Zero-padded data shares, S-pitched (zfec pads the tail with zeros):
-  // columns [off, off + cnt) of every share into pinned staging.
+  // columns [off, off + cnt) of every share into pinned staging, the bytes
+  // spread evenly over the host pool.
+  std::vector<CopySeg> segs;
   auto pack = [&](size_t off, size_t cnt) {
-    const int parts = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
-    pool.run(parts, [&](int part) {
-      for (uint32_t j = static_cast<uint32_t>(part); j < k; j += parts) {
-        const size_t src = static_cast<size_t>(j) * B + off;
-        size_t avail = off < B ? std::min(cnt, B - off) : 0;
-        avail = src < len ? std::min(avail, len - src) : 0;
-        uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(j) * S + off;
-        if (avail) std::memcpy(dst, data + src, avail);
-        if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
-      }
-    });
+    segs.clear();
+    for (uint32_t j = 0; j < k; j++) {
+      const size_t src = static_cast<size_t>(j) * B + off;
+      size_t avail = off < B ? std::min(cnt, B - off) : 0;
+      avail = src < len ? std::min(avail, len - src) : 0;
+      uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(j) * S + off;
+      if (avail) segs.push_back({dst, data + src, avail});
+      if (cnt > avail) segs.push_back({dst + avail, nullptr, cnt - avail});
+    }
+    pool.copy_segs(segs.data(), segs.size());
   };
   auto unpack = [&](size_t off, size_t cnt) {
     const size_t c = off < B ? std::min(cnt, B - off) : 0;
     if (!c) return;
-    const int parts = static_cast<size_t>(p) * c >= (2u << 20) ? static_cast<int>(p) : 1;
-    pool.run(parts, [&](int part) {
-      for (uint32_t i = static_cast<uint32_t>(part); i < p; i += parts)
-        std::memcpy(parity_out[i] + off, ctx->pin_out.p + static_cast<size_t>(i) * S + off, c);
-    });
+    segs.clear();
+    for (uint32_t i = 0; i < p; i++)
+      segs.push_back({parity_out[i] + off, ctx->pin_out.p + static_cast<size_t>(i) * S + off, c});
+    pool.copy_segs(segs.data(), segs.size());
   };
   if (zc) {  // the kernel reads and writes page-locked host memory over PCIe
     uint8_t *dd, *dp = nullptr;
@@ -181,17 +181,16 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   rc = decode_rows(ctx, k, n, slot_idx, coef, missing);
   if (rc) return rc;
   const size_t outlen = static_cast<size_t>(k) * block - padlen;
-  auto put = [&](uint32_t row, const uint8_t *src) {
-    const size_t off = static_cast<size_t>(row) * block;
-    if (off < outlen) std::memcpy(out + off, src, std::min(block, outlen - off));
-  };
   HostPool &pool = host_pool(ctx);
-  const int parts = static_cast<size_t>(k) * block >= (1u << 20) ? static_cast<int>(k) : 1;
+  std::vector<CopySeg> segs;
   auto put_present = [&] {  // surviving data shares: plain copies into out
-    pool.run(parts, [&](int part) {
-      for (uint32_t s = static_cast<uint32_t>(part); s < k; s += parts)
-        if (slot_idx[s] < k) put(s, shares[slot_pos[s]]);
-    });
+    segs.clear();
+    for (uint32_t s = 0; s < k; s++) {
+      const size_t off = static_cast<size_t>(s) * block;
+      if (slot_idx[s] < k && off < outlen)
+        segs.push_back({out + off, shares[slot_pos[s]], std::min(block, outlen - off)});
+    }
+    pool.copy_segs(segs.data(), segs.size());
   };
   if (missing.empty()) {  // all data shares present: concatenation, as zfec
     put_present();
@@ -220,28 +219,29 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
     const size_t o = static_cast<size_t>(row) * block + off;
     size_t c = off < block ? std::min(cnt, block - off) : 0;
     c = o < outlen ? std::min(c, outlen - o) : 0;
-    if (c) std::memcpy(out + o, src, c);
+    if (c) segs.push_back({out + o, src, c});
   };
   // slot shares into pinned staging; present data shares also into out
   auto pack = [&](size_t off, size_t cnt) {
-    const int pp = static_cast<size_t>(k) * cnt >= (2u << 20) ? static_cast<int>(k) : 1;
-    pool.run(pp, [&](int part) {
-      for (uint32_t c = static_cast<uint32_t>(part); c < k; c += pp) {
-        const uint8_t *src = shares[slot_pos[c]] + off;
-        const size_t avail = off < block ? std::min(cnt, block - off) : 0;
-        if (!in_direct) {
-          uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(c) * S + off;
-          if (avail) std::memcpy(dst, src, avail);
-          if (cnt > avail) std::memset(dst + avail, 0, cnt - avail);
-        }
-        if (slot_idx[c] < k) put_cols(c, off, cnt, src);
+    segs.clear();
+    for (uint32_t c = 0; c < k; c++) {
+      const uint8_t *src = shares[slot_pos[c]] + off;
+      const size_t avail = off < block ? std::min(cnt, block - off) : 0;
+      if (!in_direct) {
+        uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(c) * S + off;
+        if (avail) segs.push_back({dst, src, avail});
+        if (cnt > avail) segs.push_back({dst + avail, nullptr, cnt - avail});
       }
-    });
+      if (slot_idx[c] < k) put_cols(c, off, cnt, src);
+    }
+    pool.copy_segs(segs.data(), segs.size());
   };
   auto unpack = [&](size_t off, size_t cnt) {
     if (out_direct) return;
+    segs.clear();
     for (uint32_t r = 0; r < e; r++)
       put_cols(missing[r], off, cnt, ctx->pin_out.p + static_cast<size_t>(r) * S + off);
+    pool.copy_segs(segs.data(), segs.size());
   };
   hipStream_t s = ctx->stream;
   std::vector<const uint8_t *> in(k);

@@ -8,6 +8,8 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -18,6 +20,13 @@
 
 namespace storb_rs {
 
+// A byte range to copy (src != nullptr) or to zero-fill (src == nullptr).
+struct CopySeg {
+  uint8_t *dst;
+  const uint8_t *src;
+  size_t len;
+};
+
 class HostPool {
  public:
   explicit HostPool(int nthreads) {
@@ -26,7 +35,8 @@ class HostPool {
   ~HostPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
+      stop_.store(true);
+      gen_.fetch_add(1);
     }
     cv_.notify_all();
     for (auto &t : workers_) t.join();
@@ -37,45 +47,67 @@ class HostPool {
   int size() const { return static_cast<int>(workers_.size()) + 1; }
 
   // f(i) for every i in [0, parts); the caller takes part too. Blocking.
+  // Workers that finished a job spin for kSpinUs before sleeping, so the
+  // back-to-back jobs of one call (pack, launch, unpack of each slice) start
+  // without a futex wake-up each (~5-20 us on a busy host).
   void run(int parts, const std::function<void(int)> &f) {
     if (parts <= 0) return;
     if (parts == 1 || workers_.empty()) {
       for (int i = 0; i < parts; i++) f(i);
       return;
     }
+    bool wake;
     {
       std::lock_guard<std::mutex> lk(mu_);
       job_ = &f;
       parts_ = parts;
       next_ = 0;
-      done_ = 0;
-      gen_++;
+      done_.store(0, std::memory_order_relaxed);
+      gen_.fetch_add(1, std::memory_order_release);
+      wake = sleepers_ > 0;
     }
-    cv_.notify_all();
+    if (wake) cv_.notify_all();
     work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return done_ == parts_; });
+    for (unsigned spin = 0; done_.load(std::memory_order_acquire) != parts; spin++)
+      if (spin > 4096) std::this_thread::yield();
+    std::lock_guard<std::mutex> lk(mu_);
     job_ = nullptr;
   }
 
   // memcpy split into >= 1 MiB slices over the pool.
   void copy(void *dst, const void *src, size_t bytes) {
-    constexpr size_t kSlice = 1u << 20;
-    const int parts = static_cast<int>(std::min<size_t>(size(), (bytes + kSlice - 1) / kSlice));
-    if (parts <= 1) {
-      std::memcpy(dst, src, bytes);
-      return;
-    }
-    const size_t per = ((bytes + parts - 1) / parts + 4095) & ~static_cast<size_t>(4095);
-    run(parts, [&](int i) {
-      const size_t off = std::min(bytes, static_cast<size_t>(i) * per);
-      const size_t cnt = std::min(per, bytes - off);
-      if (cnt) std::memcpy(static_cast<uint8_t *>(dst) + off,
-                           static_cast<const uint8_t *>(src) + off, cnt);
+    CopySeg s{static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), bytes};
+    copy_segs(&s, 1, 1u << 20);
+  }
+
+  // Copy / zero-fill a list of byte ranges, the total split evenly over up
+  // to size() threads with at least min_part bytes each.
+  void copy_segs(const CopySeg *segs, size_t nsegs, size_t min_part = 64u << 10) {
+    size_t total = 0;
+    for (size_t i = 0; i < nsegs; i++) total += segs[i].len;
+    if (total == 0) return;
+    const int parts = static_cast<int>(
+        std::max<size_t>(1, std::min<size_t>(size(), total / std::max<size_t>(min_part, 1))));
+    const size_t per = ((total + parts - 1) / parts + 63) & ~static_cast<size_t>(63);
+    run(parts, [&](int p) {
+      size_t lo = std::min(total, static_cast<size_t>(p) * per), hi = std::min(total, lo + per);
+      size_t base = 0;
+      for (size_t i = 0; i < nsegs && lo < hi; i++) {
+        const CopySeg &sg = segs[i];
+        if (base + sg.len > lo) {
+          const size_t a = lo - base, b = std::min(sg.len, hi - base);
+          if (sg.src) std::memcpy(sg.dst + a, sg.src + a, b - a);
+          else std::memset(sg.dst + a, 0, b - a);
+          lo = base + b;
+        }
+        base += sg.len;
+      }
     });
   }
 
  private:
+  static constexpr int kSpinUs = 60;
+
   void work() {
     for (;;) {
       int i;
@@ -87,19 +119,29 @@ class HostPool {
         f = job_;
       }
       (*f)(i);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (++done_ == parts_) done_cv_.notify_all();
+      done_.fetch_add(1, std::memory_order_acq_rel);
     }
   }
 
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned spin = 1; gen_.load(std::memory_order_acquire) == seen; spin++) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+        if ((spin & 255) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs))
+          break;
+      }
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
+        sleepers_++;
+        cv_.wait(lk, [&] { return gen_.load() != seen; });
+        sleepers_--;
+        if (stop_.load()) return;
+        seen = gen_.load();
       }
       work();
     }
@@ -107,11 +149,12 @@ class HostPool {
 
   std::vector<std::thread> workers_;
   std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
+  std::condition_variable cv_;
   const std::function<void(int)> *job_ = nullptr;
-  int parts_ = 0, next_ = 0, done_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  int parts_ = 0, next_ = 0, sleepers_ = 0;
+  std::atomic<int> done_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
 };
 
 }  // namespace storb_rs

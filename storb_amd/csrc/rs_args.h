@@ -59,6 +59,27 @@ struct ApplyArgs {
   uint64_t copy_stride[kMaxIn];
 };
 
+// Per-stripe descriptors: one launch over stripes that each lost different
+// shares (Storb's download keeps whichever k + 1 pieces arrive first,
+// download.rs:363-451, so the survivor set varies from chunk to chunk). Item
+// i of the launch is the record desc + i * rec_qwords (8-byte words):
+//   [0]                  pattern t: its tables at ptab + t * k * tab_rows
+//   [1 .. k]             input pointers, slot order
+//   [k+1 .. k+r]         output row pointers
+//   [k+r+1 .. 2k+r]      (copy != 0) where input j is also stored, 0 = nowhere
+// Every item of a launch rebuilds r rows with its own matrix and pointers;
+// the stripes (and shares) of different items need not be related at all.
+struct DescArgs {
+  const uint64_t *desc;
+  const PermTab *ptab;
+  uint64_t block;  // bytes per share
+  uint32_t k, r;
+  uint32_t tab_rows;  // = rows_bucket(r ? r : 1)
+  uint32_t nitems;
+  uint32_t copy;
+  uint32_t rec_qwords;  // 1 + k + r (+ k with copy)
+};
+
 // Launch shape of the bit-sliced kernels (rs_bitslice_core.h), shared by
 // the host launchers and the kernels. Grid: nstripes x tiles; a tile = T
 // lanes x 32 B of every share. Wave w of the tile covers 2 KiB: lane l holds

@@ -1,7 +1,5 @@
 // rs_bitslice.hip -- instantiations of the bit-sliced encoders
 // (rs_bitslice.hpp) for Storb's wide full-chunk geometries.
-#include <cstdlib>
-
 #include "rs_bitslice.hpp"
 
 namespace storb_rs {
@@ -14,14 +12,9 @@ bool bitslice_supported(uint32_t k, uint32_t n) {
 
 hipError_t launch_encode_bitslice(const ApplyArgs &a, uint32_t n, hipStream_t s) {
   if (a.r != n - a.k || !vector_ok(a)) return hipErrorInvalidValue;
-  // STORB_RS_BS_SPLIT=1: the row-split form for (16, 24) / (32, 48) too (A/B
-  // only: two waves of 4 / 8 rows sharing planes, 6 per CU).
-  static const bool split = [] {
-    const char *e = std::getenv("STORB_RS_BS_SPLIT");
-    return e && e[0] == '1';
-  }();
-  if (split && a.k == 16 && n == 24) return bs::launch_bitslice_split<16, 24, 6>(a, s);
-  if (split && a.k == 32 && n == 48) return bs::launch_bitslice_split<32, 48, 6>(a, s);
+  // (The row-split form measured equal for (16, 24) and within noise for
+  // (32, 48) in the product, profiles/r2_k64/split_aot_k16_k32_ab.txt: one
+  // wave per tile stays.)
   if (a.k == 16 && n == 24) return bs::launch_bitslice<16, 24>(a, s);
   if (a.k == 32 && n == 48) return bs::launch_bitslice<32, 48>(a, s);
   if (a.k == 64 && n == 96) return launch_encode_bitslice_64_96(a, s);

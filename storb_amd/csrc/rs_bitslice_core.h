@@ -269,15 +269,6 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
 // bit-planes through LDS; both waves fold every input into their own rows.
 // One barrier per load group, LDS double-buffered by group parity.
 
-template <bool C, class A, class B>
-struct pick_type {
-  typedef A type;
-};
-template <class A, class B>
-struct pick_type<false, A, B> {
-  typedef B type;
-};
-
 // Rows [R0, R1) of matrix M, as a matrix type of their own.
 template <class M, int R0, int R1>
 struct RowSlice {
@@ -302,12 +293,6 @@ template <int G>
 struct SplitLds {
   v4 v[2 * 2 * (G / 2) * 2 * 64];
 };
-// Table-sharing variant (SPLIT_TAB): [group parity][owner wave][G/2 inputs][8 quads][64 lanes],
-// quad q = table entries 4q..4q+3 of lo (q < 4) / hi (q >= 4).
-template <int G>
-struct SplitTabLds {
-  v4 v[2 * 2 * (G / 2) * 8 * 64];
-};
 static_assert(sizeof(SplitLds<2>) == split_lds_bytes(2) && sizeof(SplitLds<4>) == split_lds_bytes(4),
               "rs_args.h split_lds_bytes");
 
@@ -318,7 +303,7 @@ __device__ __forceinline__ void split_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <class M, int G, int W, bool TAB = false>
+template <class M, int G, int W>
 __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t stripe, uint32_t v0,
                                               uint32_t cols, uint32_t lane, v4 *lds) {
   constexpr int K = M::K, R = M::R, H = G / 2, RA = (R + 1) / 2;
@@ -353,22 +338,10 @@ __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t strip
       asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
                    "+v"(x[6]), "+v"(x[7]));
       transpose8(x);
-      if constexpr (TAB) {
-        uint32_t lo[16], hi[16];
-        make_tables(x, lo, hi);
-        v4 *slot = lds + ((((gi & 1) * 2 + W) * H + h) * 8) * 64 + lane;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          slot[q * 64] = v4{lo[4 * q], lo[4 * q + 1], lo[4 * q + 2], lo[4 * q + 3]};
-          slot[(4 + q) * 64] = v4{hi[4 * q], hi[4 * q + 1], hi[4 * q + 2], hi[4 * q + 3]};
-        }
-        fold_tables<MW, j>(acc, lo, hi);
-      } else {
-        v4 *slot = lds + ((((gi & 1) * 2 + W) * H + h) * 2) * 64 + lane;
-        slot[0] = v4{x[0], x[1], x[2], x[3]};
-        slot[64] = v4{x[4], x[5], x[6], x[7]};
-        fold_planes<MW, j>(acc, x);
-      }
+      v4 *slot = lds + ((((gi & 1) * 2 + W) * H + h) * 2) * 64 + lane;
+      slot[0] = v4{x[0], x[1], x[2], x[3]};
+      slot[64] = v4{x[4], x[5], x[6], x[7]};
+      fold_planes<MW, j>(acc, x);
       fence_acc(acc);
     });
     split_barrier();
@@ -376,22 +349,10 @@ __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t strip
     static_for<H>([&](auto HH) {
       constexpr int h = decltype(HH)::value;
       constexpr int j = gi * G + (1 - W) * H + h;
-      if constexpr (TAB) {
-        const v4 *slot = lds + ((((gi & 1) * 2 + (1 - W)) * H + h) * 8) * 64 + lane;
-        uint32_t lo[16], hi[16];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const v4 L = slot[q * 64], Hq = slot[(4 + q) * 64];
-          lo[4 * q] = L[0], lo[4 * q + 1] = L[1], lo[4 * q + 2] = L[2], lo[4 * q + 3] = L[3];
-          hi[4 * q] = Hq[0], hi[4 * q + 1] = Hq[1], hi[4 * q + 2] = Hq[2], hi[4 * q + 3] = Hq[3];
-        }
-        fold_tables<MW, j>(acc, lo, hi);
-      } else {
-        const v4 *slot = lds + ((((gi & 1) * 2 + (1 - W)) * H + h) * 2) * 64 + lane;
-        const v4 P = slot[0], Q = slot[64];
-        uint32_t x[8] = {P[0], P[1], P[2], P[3], Q[0], Q[1], Q[2], Q[3]};
-        fold_planes<MW, j>(acc, x);
-      }
+      const v4 *slot = lds + ((((gi & 1) * 2 + (1 - W)) * H + h) * 2) * 64 + lane;
+      const v4 P = slot[0], Q = slot[64];
+      uint32_t x[8] = {P[0], P[1], P[2], P[3], Q[0], Q[1], Q[2], Q[3]};
+      fold_planes<MW, j>(acc, x);
       fence_acc(acc);
     });
   });
@@ -409,10 +370,11 @@ __device__ __forceinline__ void bs_split_wave(const ApplyArgs &a, uint32_t strip
 }
 
 // Grid: nstripes x tiles of kSplitColsPerTile columns, kSplitThreads lanes.
-// TAB: share the Four-Russians tables instead of the planes (tools/k64split.hip A/B).
-template <class M, int G, int SWZ = 0, bool TAB = false>
+// (Sharing the Four-Russians tables instead of the planes measured slower,
+// 366.9 -> 387.9 us at k = 64, profiles/r2_k64/k64split_tables.txt; removed.)
+template <class M, int G, int SWZ = 0>
 __device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
-  __shared__ typename pick_type<TAB, SplitTabLds<G>, SplitLds<G>>::type lds;
+  __shared__ SplitLds<G> lds;
   constexpr uint32_t CPT = kSplitColsPerTile;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + CPT - 1) / CPT;
@@ -423,9 +385,9 @@ __device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
   const uint32_t v0 = tile * CPT + lane;
   // wave-uniform (an SGPR), so the two row halves are scalar branches
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0)
-    bs_split_wave<M, G, 0, TAB>(a, stripe, v0, cols, lane, lds.v);
+    bs_split_wave<M, G, 0>(a, stripe, v0, cols, lane, lds.v);
   else
-    bs_split_wave<M, G, 1, TAB>(a, stripe, v0, cols, lane, lds.v);
+    bs_split_wave<M, G, 1>(a, stripe, v0, cols, lane, lds.v);
 }
 
 template <class M, int G, int T = kBsThreads, int SWZ = 0>

@@ -118,20 +118,55 @@ __device__ __forceinline__ void st_stream(u32x4 *p, u32x4 v) {
 #endif
 }
 
+// Where a tile's shares are: the pointers of input j, output row i and the
+// assembly target of input j for the stripe a workgroup works on.
+// ArgsView: one matrix and one stride per slot for every stripe of the
+// launch (ApplyArgs); DescView: the stripe's own record (DescArgs), for
+// launches whose stripes each lost different shares.
+struct ArgsView {
+  const ApplyArgs &a;
+  uint32_t stripe;
+  __device__ __forceinline__ const uint8_t *in(int j) const {
+    return a.in[j] + static_cast<uint64_t>(stripe) * a.in_stride[j];
+  }
+  __device__ __forceinline__ uint8_t *out(int i) const {
+    return a.out[i] + static_cast<uint64_t>(stripe) * a.out_stride[i];
+  }
+  __device__ __forceinline__ bool has_copy(int j) const { return a.copy[j] != nullptr; }
+  __device__ __forceinline__ uint8_t *copy(int j) const {
+    return a.copy[j] + static_cast<uint64_t>(stripe) * a.copy_stride[j];
+  }
+  __device__ __forceinline__ bool accumulate() const { return a.accumulate != 0; }
+};
+
+struct DescView {
+  const uint64_t *rec;  // this item's record (wave-uniform: scalar loads)
+  uint32_t k, r;
+  __device__ __forceinline__ const uint8_t *in(int j) const {
+    return reinterpret_cast<const uint8_t *>(rec[1 + j]);
+  }
+  __device__ __forceinline__ uint8_t *out(int i) const {
+    return reinterpret_cast<uint8_t *>(rec[1 + k + i]);
+  }
+  __device__ __forceinline__ bool has_copy(int j) const { return rec[1 + k + r + j] != 0; }
+  __device__ __forceinline__ uint8_t *copy(int j) const {
+    return reinterpret_cast<uint8_t *>(rec[1 + k + r + j]);
+  }
+  __device__ __forceinline__ bool accumulate() const { return false; }
+};
+
 // Inputs are consumed in groups of up to 8 shares; the next group's
 // dwordx4 loads are issued before the current group is multiplied (double
 // buffer), so a k = 32 tile needs 2 x 8 input registers per column instead
 // of 32.
-template <int KM, int G, int T, int U, bool GUARD>
-__device__ __forceinline__ void load_group(const ApplyArgs &a, uint32_t k, uint32_t cols,
-                                           uint32_t stripe, uint32_t c0, int g,
-                                           u32x4 (&dst)[G][U]) {
+template <int KM, int G, int T, int U, bool GUARD, class V>
+__device__ __forceinline__ void load_group(const V &v, uint32_t k, uint32_t cols, uint32_t c0,
+                                           int g, u32x4 (&dst)[G][U]) {
 #pragma unroll
   for (int jj = 0; jj < G; jj++) {
     const int j = g * G + jj;
     if (j >= static_cast<int>(k)) continue;
-    const u32x4 *p = reinterpret_cast<const u32x4 *>(
-        a.in[j] + static_cast<uint64_t>(stripe) * a.in_stride[j]);
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(v.in(j));
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t c = c0 + u * T;
@@ -152,16 +187,14 @@ __device__ __forceinline__ void load_group(const ApplyArgs &a, uint32_t k, uint3
 // surviving data share straight from the registers it was loaded into, so
 // the chunk is assembled in the same pass (k*B read + k*B written instead of
 // a separate copy pass re-reading the k - e present shares).
-template <int G, int T, int U, bool GUARD>
-__device__ __forceinline__ void copy_group(const ApplyArgs &a, uint32_t k, uint32_t cols,
-                                           uint32_t stripe, uint32_t c0, int g,
-                                           const u32x4 (&src)[G][U]) {
+template <int G, int T, int U, bool GUARD, class V>
+__device__ __forceinline__ void copy_group(const V &v, uint32_t k, uint32_t cols, uint32_t c0,
+                                           int g, const u32x4 (&src)[G][U]) {
 #pragma unroll
   for (int jj = 0; jj < G; jj++) {
     const int j = g * G + jj;
-    if (j >= static_cast<int>(k) || a.copy[j] == nullptr) continue;
-    u32x4 *q = reinterpret_cast<u32x4 *>(a.copy[j] + static_cast<uint64_t>(stripe) *
-                                                         a.copy_stride[j]);
+    if (j >= static_cast<int>(k) || !v.has_copy(j)) continue;
+    u32x4 *q = reinterpret_cast<u32x4 *>(v.copy(j));
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t c = c0 + u * T;
@@ -171,10 +204,9 @@ __device__ __forceinline__ void copy_group(const ApplyArgs &a, uint32_t k, uint3
 }
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD,
-          bool COPY = false>
-__device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tabs,
-                                          uint32_t k, uint32_t r, uint32_t cols,
-                                          uint32_t stripe, uint32_t c0) {
+          bool COPY = false, class V>
+__device__ __forceinline__ void perm_tile(const V &v, const PermTab *tabs, uint32_t k,
+                                          uint32_t r, uint32_t cols, uint32_t c0) {
   constexpr int NG = KM / G;
   u32x4 buf[2][G][U];
   u32x4 acc[RM][U];
@@ -183,13 +215,13 @@ __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tab
 #pragma unroll
     for (int u = 0; u < U; u++) acc[i][u] = u32x4{0, 0, 0, 0};
 
-  load_group<KM, G, T, U, GUARD>(a, k, cols, stripe, c0, 0, buf[0]);
+  load_group<KM, G, T, U, GUARD>(v, k, cols, c0, 0, buf[0]);
 #pragma unroll
   for (int g = 0; g < NG; g++) {
     if (g + 1 < NG)
-      load_group<KM, G, T, U, GUARD>(a, k, cols, stripe, c0, g + 1, buf[(g + 1) & 1]);
+      load_group<KM, G, T, U, GUARD>(v, k, cols, c0, g + 1, buf[(g + 1) & 1]);
     if constexpr (COPY) {
-      copy_group<G, T, U, GUARD>(a, k, cols, stripe, c0, g, buf[g & 1]);
+      copy_group<G, T, U, GUARD>(v, k, cols, c0, g, buf[g & 1]);
       if (r == 0) continue;  // pure assembly: nothing missing
     }
     if constexpr (PAIR) {
@@ -271,15 +303,14 @@ __device__ __forceinline__ void perm_tile(const ApplyArgs &a, const PermTab *tab
 #pragma unroll
   for (int i = 0; i < RM; i++) {
     if (i >= static_cast<int>(r)) continue;
-    u32x4 *q = reinterpret_cast<u32x4 *>(
-        a.out[i] + static_cast<uint64_t>(stripe) * a.out_stride[i]);
+    u32x4 *q = reinterpret_cast<u32x4 *>(v.out(i));
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t c = c0 + u * T;
       if (!GUARD || c < cols) {
-        u32x4 v = acc[i][u];
-        if (a.accumulate) v ^= q[c];
-        st_stream(q + c, v);
+        u32x4 x = acc[i][u];
+        if (v.accumulate()) x ^= q[c];
+        st_stream(q + c, x);
       }
     }
   }
@@ -306,11 +337,43 @@ __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
     __syncthreads();
     tabs = lds_ptab;
   }
+  const ArgsView v{a, stripe};
   if (base + TILE <= cols)
-    perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(a, tabs, a.k, a.r, cols, stripe,
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, a.r, cols,
                                                       base + threadIdx.x);
   else
-    perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(a, tabs, a.k, a.r, cols, stripe,
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, a.r, cols,
+                                                     base + threadIdx.x);
+}
+
+// The same tile for a launch of per-stripe descriptors (DescArgs): item
+// blockIdx / tiles-per-share reads its record -- the inputs, outputs and
+// assembly targets of its own stripe and the tables of its own matrix --
+// with scalar loads, then runs perm_tile exactly as rs_apply_perm does.
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false,
+          bool COPY = false>
+__global__ __launch_bounds__(T) void rs_apply_desc(const DescArgs a) {
+  constexpr uint32_t TILE = T * U;
+  const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
+  const uint32_t tps = (cols + TILE - 1) / TILE;
+  const uint32_t item = blockIdx.x / tps;
+  const uint32_t base = (blockIdx.x - item * tps) * TILE;
+  const uint64_t *rec = a.desc + static_cast<uint64_t>(item) * a.rec_qwords;
+  const PermTab *tabs = a.ptab + static_cast<uint64_t>(rec[0] & 0xFFFFFFFFu) * a.k * RM;
+  if constexpr (TL) {
+    __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * RM];
+    const uint32_t n16 = (COPY && a.r == 0) ? 0u : a.k * RM * (sizeof(PermTab) / 16);
+    for (uint32_t t = threadIdx.x; t < n16; t += T)
+      reinterpret_cast<u32x4 *>(lds_ptab)[t] = reinterpret_cast<const u32x4 *>(tabs)[t];
+    __syncthreads();
+    tabs = lds_ptab;
+  }
+  const DescView v{rec, a.k, a.r};
+  if (base + TILE <= cols)
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, a.r, cols,
+                                                      base + threadIdx.x);
+  else
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, a.r, cols,
                                                      base + threadIdx.x);
 }
 
@@ -330,6 +393,51 @@ hipError_t launch_perm(const ApplyArgs &a, hipStream_t s, int occ = 0, int occ_c
       return hipErrorInvalidValue;
   }
   return launch_lds<rs_apply_perm<KM, RM, T, U, BAR, G, TL, PAIR>>(blocks, T, dyn, s, a);
+}
+
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
+hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_copy = 0) {
+  const uint64_t cols = a.block >> 4;
+  const uint64_t blocks = ((cols + T * U - 1) / (T * U)) * a.nitems;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+  const size_t dyn = cap_lds(wg_cap(a.copy ? occ_copy : occ),
+                             TL ? sizeof(PermTab) * KM * RM : 0);
+  if (a.copy) {
+    if constexpr (KM <= static_cast<int>(kCopyMaxK))
+      return launch_lds<rs_apply_desc<KM, RM, T, U, BAR, G, TL, PAIR, true>>(blocks, T, dyn, s,
+                                                                             a);
+    else
+      return hipErrorInvalidValue;
+  }
+  return launch_lds<rs_apply_desc<KM, RM, T, U, BAR, G, TL, PAIR>>(blocks, T, dyn, s, a);
+}
+
+template <int KM>
+hipError_t go_desc_r(const DescArgs &a, hipStream_t s) {
+  switch (rows_bucket(a.r)) {
+#define STORB_DESC_CASE(R)                                                                 \
+  case R: {                                                                                \
+    using C = Tune<KM, R>;                                                                 \
+    return launch_desc<KM, R, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC,      \
+                                                                        C::OCC_COPY);      \
+  }
+    case 0:  // pure assembly (COPY, nothing missing): one zero row of tables
+      STORB_DESC_CASE(1)
+      STORB_DESC_CASE(2)
+      STORB_DESC_CASE(3)
+      STORB_DESC_CASE(4)
+      STORB_DESC_CASE(5)
+      STORB_DESC_CASE(6)
+      STORB_DESC_CASE(7)
+      STORB_DESC_CASE(8)
+#undef STORB_DESC_CASE
+    default: {
+      using C = Tune<KM, 16>;
+      return launch_desc<KM, 16, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC,
+                                                                           C::OCC_COPY);
+    }
+  }
 }
 
 template <int KM, int RM>
@@ -415,25 +523,9 @@ inline uint64_t tile_blocks(const ApplyArgs &a) {
   return ((cols + TILE - 1) / TILE) * a.nstripes;
 }
 
-// Buckets the benches run that can also launch with 64- or 128-lane
-// workgroups (STORB_RS_TABLE_T, rs_kernels.hpp; the cap scaled to the same
-// waves per CU) for launch-shape A/B in the product.
-template <int KM, int RM>
-constexpr bool kAltThreads = (KM == 4 && RM <= 2) || (KM == 8 && (RM == 3 || RM == 4)) ||
-                             (KM == 2 && RM == 1) || (KM == 16 && RM <= 2);
-
 template <int KM, int RM>
 hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
   using C = Tune<KM, RM>;
-  if constexpr (kAltThreads<KM, RM>) {
-    const int t = table_threads_override();
-    if (t == 64)
-      return launch_perm<KM, RM, 64, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC * 4,
-                                                                        C::OCC_COPY * 4);
-    if (t == 128)
-      return launch_perm<KM, RM, 128, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC * 2,
-                                                                         C::OCC_COPY * 2);
-  }
   return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC, C::OCC_COPY);
 }
 
@@ -462,5 +554,11 @@ hipError_t dispatch_perm_k8(const ApplyArgs &a, hipStream_t s);
 hipError_t dispatch_perm_k16(const ApplyArgs &a, hipStream_t s);
 hipError_t dispatch_perm_k32(const ApplyArgs &a, hipStream_t s);
 hipError_t dispatch_lds(const ApplyArgs &a, hipStream_t s);
+hipError_t dispatch_desc_k1(const DescArgs &a, hipStream_t s);
+hipError_t dispatch_desc_k2(const DescArgs &a, hipStream_t s);
+hipError_t dispatch_desc_k4(const DescArgs &a, hipStream_t s);
+hipError_t dispatch_desc_k8(const DescArgs &a, hipStream_t s);
+hipError_t dispatch_desc_k16(const DescArgs &a, hipStream_t s);
+hipError_t dispatch_desc_k32(const DescArgs &a, hipStream_t s);
 
 }  // namespace storb_rs

@@ -11,9 +11,13 @@
 // writes the matrix out as a constexpr table and compiles the same core
 // header with hipRTC, once per (matrix, copy mask), on a background thread.
 // Calls that arrive while a kernel compiles run the table kernel
-// (STORB_RS_JIT=sync waits instead); compiled kernels stay loaded for the
-// life of the process (never unloaded, so no queued launch can outlive its
-// code object), at most STORB_RS_JIT_MAX of them (default 256).
+// (STORB_RS_JIT=sync waits instead). A matrix is compiled only once it has
+// been asked for twice (a pattern one chunk of a download uses is not worth
+// a compile); at most STORB_RS_JIT_MAX kernels (default 256) are loaded, the
+// least recently used one unloaded for a new one once every launch of it
+// has completed (per-stream launch events), so no queued launch can outlive
+// its code object. One compile thread, at a lower CPU priority than the
+// host copy workers it shares the CPUs with.
 #include <hip/hip_runtime_api.h>
 #include <hip/hiprtc.h>
 
@@ -29,7 +33,12 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
+
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../../include/storb_rs.h"
 #include "gf256.hpp"
@@ -45,26 +54,29 @@ namespace {
 // ahead-of-time kernels).
 #include "jit_headers.inc"
 
-enum class Mode { Off, Async, Sync };
+enum class Mode { Off, Async, Sync, Always };
 
-// STORB_RS_JIT: unset / 1 = async, sync, 0 = off; "always" (measurements
-// only) = sync and every k >= 8 matrix, VALU-bound on the table kernel or not.
-Mode mode() {
+// STORB_RS_JIT (read once): unset / 1 = async, sync, 0 = off; "always"
+// (measurements only) = sync and every k >= 8 matrix, VALU-bound on the
+// table kernel or not.
+Mode raw_mode() {
   static const Mode m = [] {
     const char *e = std::getenv("STORB_RS_JIT");
     if (!e || !*e) return Mode::Async;
-    if (std::strcmp(e, "sync") == 0 || std::strcmp(e, "always") == 0) return Mode::Sync;
+    if (std::strcmp(e, "always") == 0) return Mode::Always;
+    if (std::strcmp(e, "sync") == 0) return Mode::Sync;
     return std::atoi(e) ? Mode::Async : Mode::Off;
   }();
   return m;
 }
+Mode mode() { return raw_mode() == Mode::Always ? Mode::Sync : raw_mode(); }
+bool always() { return raw_mode() == Mode::Always; }
 
-bool always() {
-  static const bool a = [] {
-    const char *e = std::getenv("STORB_RS_JIT");
-    return e && std::strcmp(e, "always") == 0;
-  }();
-  return a;
+// STORB_RS_JIT_DUMP=dir: write every compiled kernel's source and code
+// object there (and a failed compile's log to stderr).
+const char *dump_dir() {
+  static const char *d = std::getenv("STORB_RS_JIT_DUMP");
+  return d && *d ? d : nullptr;
 }
 
 size_t max_kernels() {
@@ -84,7 +96,16 @@ struct Entry {
   std::vector<char> code;
   std::string log;
   std::map<int, hipFunction_t> fn;  // per device
-  std::vector<hipModule_t> modules;
+  std::vector<std::pair<int, hipModule_t>> modules;  // (device, module)
+  // Last launch on each (device, stream): the entry may be unloaded once all
+  // have completed.
+  struct Use {
+    int device;
+    hipStream_t stream;
+    hipEvent_t done;
+  };
+  std::vector<Use> uses;
+  uint64_t tick = 0;  // LRU clock
 };
 
 class Jit;
@@ -120,19 +141,30 @@ class Jit {
     if (w.joinable()) w.join();
   }
 
-  // The entry for key, created and queued for compilation if new (nullptr
-  // when the kernel budget is spent); src() writes the kernel source (symbol
-  // `name`), only for a new entry. In Sync mode waits for the compile.
+  // The entry for key, created and queued for compilation if new; src()
+  // writes the kernel source (symbol `name`), only for a new entry. nullptr
+  // (the caller runs the table kernel): a matrix asked for the first time
+  // (unless `force`, or in Sync mode), or no room -- STORB_RS_JIT_MAX loaded
+  // and none of them idle. In Sync mode waits for the compile.
   template <typename Src>
-  std::shared_ptr<Entry> get(const std::string &key, const std::string &name, int opt, Src &&src) {
+  std::shared_ptr<Entry> get(const std::string &key, const std::string &name, int opt, Src &&src,
+                             bool force) {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = entries_.find(key);
     std::shared_ptr<Entry> e;
     if (it != entries_.end()) {
       e = it->second;
+      e->tick = ++tick_;
     } else {
-      if (entries_.size() >= max_kernels() || stop_) return nullptr;  // budget spent / exiting
+      if (stop_) return nullptr;
+      if (!force && mode() != Mode::Sync) {
+        if (seen_.size() > (1u << 16)) seen_.clear();
+        if (++seen_[key] < 2) return nullptr;
+      }
+      if (entries_.size() >= max_kernels() && !evict_one_locked()) return nullptr;
+      seen_.erase(key);
       e = std::make_shared<Entry>();
+      e->tick = ++tick_;
       e->src = src();
       e->name = name;
       e->opt = opt;
@@ -163,10 +195,24 @@ class Jit {
     if (r != hipSuccess) return r;
     r = hipModuleGetFunction(f, m, e.name.c_str());
     if (r != hipSuccess) return r;
-    e.modules.push_back(m);
+    e.modules.emplace_back(device, m);
     e.fn[device] = *f;
     return hipSuccess;
   }
+
+  // After launching e on stream s of `device` (current): record the launch.
+  hipError_t used(Entry &e, int device, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto &u : e.uses)
+      if (u.device == device && u.stream == s) return hipEventRecord(u.done, s);
+    Entry::Use u{device, s, nullptr};
+    hipError_t r = hipEventCreateWithFlags(&u.done, hipEventDisableTiming);
+    if (r != hipSuccess) return r;
+    e.uses.push_back(u);
+    return hipEventRecord(u.done, s);
+  }
+
+
 
   void wait_for(const Entry &e) {
     std::unique_lock<std::mutex> lk(mu_);
@@ -186,12 +232,44 @@ class Jit {
     s->launches = launches;
     s->fallbacks = fallbacks;
     s->compile_ms = compile_ms_;
+    s->evicted = evicted_;
+    s->loaded = entries_.size();
   }
 
   std::atomic<uint64_t> launches{0}, fallbacks{0};
 
  private:
+  // Unload the least recently used compiled kernel that nobody holds and
+  // whose launches have all completed. Under mu_.
+  bool evict_one_locked() {
+    auto victim = entries_.end();
+    for (auto it = entries_.begin(); it != entries_.end(); ++it) {
+      const Entry &e = *it->second;
+      if (e.state == Entry::Pending || it->second.use_count() > 1) continue;
+      if (victim != entries_.end() && victim->second->tick <= e.tick) continue;
+      bool idle = true;
+      for (const auto &u : e.uses) idle = idle && hipEventQuery(u.done) == hipSuccess;
+      if (idle) victim = it;
+    }
+    if (victim == entries_.end()) return false;
+    Entry &e = *victim->second;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    for (auto &dm : e.modules) {
+      (void)hipSetDevice(dm.first);
+      (void)hipModuleUnload(dm.second);
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    for (auto &u : e.uses) (void)hipEventDestroy(u.done);
+    entries_.erase(victim);
+    evicted_++;
+    return true;
+  }
+
   void run() {
+    // Below the host copy workers (same CPUs, cgroup quota): a compile must
+    // not slow the copies of the calls running meanwhile on the table kernel.
+    (void)setpriority(PRIO_PROCESS, static_cast<id_t>(syscall(SYS_gettid)), 10);
     for (;;) {
       std::shared_ptr<Entry> e;
       {
@@ -217,9 +295,8 @@ class Jit {
         compile_ms_ += ms;
         pending_--;
       }
-      if (!ok && std::getenv("STORB_RS_JIT_VERBOSE"))
-        std::fprintf(stderr, "storb_rs jit: compile failed:\n%s\n", e->log.c_str());
-      if (const char *dir = std::getenv("STORB_RS_JIT_DUMP")) {  // inspect with hipcc -S
+      if (const char *dir = dump_dir()) {  // inspect with hipcc -S
+        if (!ok) std::fprintf(stderr, "storb_rs jit: compile failed:\n%s\n", e->log.c_str());
         const std::string path = std::string(dir) + "/storb_bs_jit_" +
                                  std::to_string(compiled_ + failed_) + ".hip";
         if (FILE *f = std::fopen(path.c_str(), "w")) {
@@ -277,6 +354,8 @@ class Jit {
   std::mutex mu_;
   std::condition_variable cv_;
   std::map<std::string, std::shared_ptr<Entry>> entries_;
+  std::unordered_map<std::string, uint32_t> seen_;  // asked-for counts of keys not compiled
+  uint64_t tick_ = 0, evicted_ = 0;
   std::deque<std::shared_ptr<Entry>> queue_;
   std::thread worker_;
   bool stop_ = false;
@@ -292,27 +371,18 @@ Jit &jit() {
 // Launch shape (rs_args.h bs_shape, shared with the ahead-of-time
 // encoders); the resident-workgroup cap is an LDS reservation
 // (rs_kernels.hpp cap_lds, see dynamic_lds()).
-// STORB_RS_JIT_SHAPE="threads,swz,cap" overrides it for every compiled
-// kernel (launch-shape A/B on the real decode path without a rebuild).
+// (Round 2 swept it on the real decode path with a run-time override,
+// tools/shape_ab.sh, profiles/r2_shape_ab/; the override is gone.)
 bs::BsShape shape(uint32_t k, uint32_t r) {
-  bs::BsShape s = bs::bs_shape(static_cast<int>(k), static_cast<int>(r));
-  if (const char *e = std::getenv("STORB_RS_JIT_SHAPE")) {
-    int t = 0, w = 0, c = 0;
-    if (std::sscanf(e, "%d,%d,%d", &t, &w, &c) == 3 && (t == 64 || t == 128 || t == 256) &&
-        (w == 0 || w == 1) && c >= 0 && c <= 32)
-      s = bs::BsShape{t, w, c};
-  }
-  s.cap = wg_cap(s.cap);
-  return s;
+  return bs::bs_shape(static_cast<int>(k), static_cast<int>(r));
 }
 
 bool split_rows(uint32_t k, uint32_t rows);
 
-// The row-split kernels' shape (rs_args.h bs_split_cap; the cap alone follows
-// STORB_RS_WG_PER_CU), or shape().
+// The row-split kernels' shape (rs_args.h bs_split_cap), or shape().
 bs::BsShape split_or_shape(uint32_t k, uint32_t r) {
   if (!split_rows(k, r)) return shape(k, r);
-  return bs::BsShape{bs::kSplitThreads, 0, wg_cap(bs::bs_split_cap(static_cast<int>(r)))};
+  return bs::BsShape{bs::kSplitThreads, 0, bs::bs_split_cap(static_cast<int>(r))};
 }
 
 // The cap's LDS reservation is requested at launch (dynamic LDS) when it is
@@ -322,14 +392,8 @@ bs::BsShape split_or_shape(uint32_t k, uint32_t r) {
 // VGPRs, and it did: the k = 64 row-split encode took 256 VGPRs with 7
 // spilled (0.535 ms in bench --config 7) against 197 and none with the same
 // reservation made at launch (0.349 ms in tools/k64split.hip); likewise the
-// 16-row blocks 229 vs 196. STORB_RS_JIT_STATIC_LDS=1 keeps it static (A/B).
-size_t dynamic_lds(size_t lds) {
-  static const bool force_static = [] {
-    const char *e = std::getenv("STORB_RS_JIT_STATIC_LDS");
-    return e && e[0] == '1';
-  }();
-  return !force_static && lds <= (64u << 10) ? lds : 0;
-}
+// 16-row blocks 229 vs 196 (profiles/r2_k64/split_dynlds_ab.txt).
+size_t dynamic_lds(size_t lds) { return lds <= (64u << 10) ? lds : 0; }
 
 // -O level of a k-input kernel. -O3 up to k = 16 (sub-second compiles); -O1
 // above, where -O3's middle end costs seconds per new pattern (the calls
@@ -341,14 +405,7 @@ size_t dynamic_lds(size_t lds) {
 // k = 32 16-lost and k = 64 32-lost decodes equal (0.2720 / 0.2717 ms, 0.370
 // / 0.368), compiles 1.1 vs 2.8 s and 5-6 vs 11.3 s; at k = 16 -O1 was 1.4-2.3 %
 // slower (decode 0.1910 vs 0.1867 ms) for 0.4 s of compile saved, so -O3 there.
-// STORB_RS_JIT_OPT=0..3 forces a level (A/B).
-int opt_level(uint32_t k) {
-  static const int forced = [] {
-    const char *e = std::getenv("STORB_RS_JIT_OPT");
-    return e && e[0] >= '0' && e[0] <= '3' && !e[1] ? e[0] - '0' : -1;
-  }();
-  return forced >= 0 ? forced : (k > 16 ? 1 : 3);
-}
+int opt_level(uint32_t k) { return k > 16 ? 1 : 3; }
 
 // Kernel symbol, so profiles tell the compiled kernels apart (bench.py and
 // profiles/summarize.py match on the "storb_bs_jit_k<k>_r<rows>_" prefix).
@@ -361,17 +418,10 @@ std::string kernel_name(uint32_t k, uint32_t rows, uint64_t copy_mask) {
 // bs_split_body: each input read and bit-sliced once, its planes shared by
 // the two row-half waves through LDS) instead of row blocks of <= kSlotR
 // that each re-read every input (rs_args.h bs_split). Needs an even k (one
-// input per wave per load group). STORB_RS_JIT_SPLIT=0 restores the row
-// blocks (A/B).
-bool split_on() {
-  static const bool on = [] {
-    const char *e = std::getenv("STORB_RS_JIT_SPLIT");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
+// input per wave per load group). Row blocks measured 0.49 vs 0.35 ms for
+// the k = 64 encode (profiles/r2_k64/k64split.txt).
 bool split_rows(uint32_t k, uint32_t rows) {
-  return split_on() && rows <= kMaxRows && bs::bs_split(static_cast<int>(k), static_cast<int>(rows));
+  return rows <= kMaxRows && bs::bs_split(static_cast<int>(k), static_cast<int>(rows));
 }
 
 // The kernel source for a (rows x k) matrix: bit b' of row[p][j][b] is bit b
@@ -450,7 +500,7 @@ bool wanted(uint32_t k, uint32_t rows, uint64_t bytes) {
 // The cache entry of a (k x r) matrix with the given copy mask: looked up,
 // or created and queued. wait: block until its compile has finished.
 static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *coef,
-                                        uint64_t copy_mask, bool wait) {
+                                        uint64_t copy_mask, bool wait, bool force) {
   const bool split = split_rows(k, r);
   const int group = split ? bs::kSplitGroup : bs::bs_group(static_cast<int>(k), static_cast<int>(r));
   const bs::BsShape sh = split_or_shape(k, r);
@@ -464,7 +514,7 @@ static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *c
   std::memcpy(&key[32], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
   auto e = J.get(key, kernel_name(k, r, copy_mask), opt_level(k),
-                 [&] { return source(k, r, coef, copy_mask, group, sh, lds, split); });
+                 [&] { return source(k, r, coef, copy_mask, group, sh, lds, split); }, force);
   if (e && wait) J.wait_for(*e);
   return e;
 }
@@ -509,7 +559,7 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
   for (uint32_t b = 0; b < nb; b++) {
     const uint32_t r0 = row_start(a.k, a.r, b), rr = row_start(a.k, a.r, b + 1) - r0;
     es[b] = entry_for(a.k, rr, coef + static_cast<size_t>(r0) * a.k, b == 0 ? copy_mask : 0,
-                      false);
+                      false, false);
     ready = ready && es[b] && es[b]->state == Entry::Ready;
   }
   if (!ready) {
@@ -550,6 +600,7 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
     r = hipModuleLaunchKernel(fs[b], static_cast<unsigned>(blocks), 1, 1,
                               static_cast<unsigned>(sh.threads), 1, 1,
                               static_cast<unsigned>(dynamic_lds(lds)), s, params, nullptr);
+    if (r == hipSuccess) r = J.used(*es[b], device, s);
     if (r == hipSuccess) J.launches++;
   }
   if (r != hipSuccess) return r;
@@ -562,7 +613,8 @@ int prepare(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask, 
   int res = 1;
   for (uint32_t b = 0; b < row_blocks(k, rows); b++) {
     const uint32_t r0 = row_start(k, rows, b), rr = row_start(k, rows, b + 1) - r0;
-    auto e = entry_for(k, rr, coef + static_cast<size_t>(r0) * k, b == 0 ? copy_mask : 0, wait);
+    auto e = entry_for(k, rr, coef + static_cast<size_t>(r0) * k, b == 0 ? copy_mask : 0, wait,
+                       true);
     if (!e) return 0;
     if (e->state == Entry::Failed) return -1;
     if (e->state != Entry::Ready) res = 0;

@@ -71,23 +71,6 @@ __global__ __launch_bounds__(kThreads) void fill_splitmix_kernel(
   }
 }
 
-int wg_cap_override() {
-  static const int v = [] {
-    const char *e = std::getenv("STORB_RS_WG_PER_CU");
-    return e && *e ? std::atoi(e) : -1;
-  }();
-  return v;
-}
-
-int table_threads_override() {
-  static const int v = [] {
-    const char *e = std::getenv("STORB_RS_TABLE_T");
-    const int t = e && *e ? std::atoi(e) : 0;
-    return (t == 64 || t == 128) ? t : 0;
-  }();
-  return v;
-}
-
 bool vector_ok(const ApplyArgs &a) {
   if (a.block % 16) return false;
   for (uint32_t j = 0; a.ncopy && j < a.k; j++)
@@ -127,6 +110,23 @@ hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s) {
     case 8: return dispatch_perm_k8(a, s);
     case 16: return dispatch_perm_k16(a, s);
     default: return dispatch_perm_k32(a, s);
+  }
+}
+
+hipError_t launch_apply_desc(const DescArgs &a, hipStream_t s) {
+  if (a.k == 0 || a.k > kSlotK || a.r > kSlotR || (a.copy && a.k > kCopyMaxK) ||
+      (a.r == 0 && !a.copy) || a.block % 16 ||
+      a.tab_rows != static_cast<uint32_t>(rows_bucket(a.r ? a.r : 1)) ||
+      a.rec_qwords != 1 + a.k + a.r + (a.copy ? a.k : 0))
+    return hipErrorInvalidValue;
+  if (a.block == 0 || a.nitems == 0) return hipSuccess;
+  switch (pow2_bucket(a.k)) {
+    case 1: return dispatch_desc_k1(a, s);
+    case 2: return dispatch_desc_k2(a, s);
+    case 4: return dispatch_desc_k4(a, s);
+    case 8: return dispatch_desc_k8(a, s);
+    case 16: return dispatch_desc_k16(a, s);
+    default: return dispatch_desc_k32(a, s);
   }
 }
 

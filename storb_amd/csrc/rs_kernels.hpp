@@ -31,16 +31,10 @@ enum class Variant { Perm = 1, Lds = 2 };
 // capping the resident workgroups streams faster (tools/kbench_tune.hip
 // "occ", profiles/r1_occupancy.txt). The cap is imposed by reserving LDS:
 // a workgroup asks for 160 KiB / cap, so cap fit on a CU and cap + 1 do not.
-// STORB_RS_WG_PER_CU overrides every kernel's cap (0 = uncapped).
+// (The caps were swept in round 1 with a run-time override,
+// tools/occ_sweep.py, profiles/r1_occupancy.txt; the override is gone.)
 constexpr size_t kLdsPerCu = 160u << 10;
-int wg_cap_override();  // -1 when unset
-// STORB_RS_TABLE_T = 64 / 128: lanes per workgroup of the table kernel's
-// benchmarked buckets (rs_device.hpp go_perm), for A/B; 0 when unset.
-int table_threads_override();
-inline int wg_cap(int tuned) {
-  const int o = wg_cap_override();
-  return o >= 0 ? o : tuned;
-}
+inline int wg_cap(int tuned) { return tuned; }
 // Dynamic LDS to request so at most `cap` workgroups with `static_lds`
 // bytes of static LDS each are resident on a CU (0 = no cap).
 inline size_t cap_lds(int cap, size_t static_lds) {
@@ -52,9 +46,9 @@ inline size_t cap_lds(int cap, size_t static_lds) {
 #ifdef __HIPCC__
 // Launch kernel Kern with `dyn` bytes of dynamic LDS (the resident-workgroup
 // cap); above 64 KiB each kernel must opt in once.
-template <auto Kern>
+template <auto Kern, class Args>
 hipError_t launch_lds(uint64_t blocks, int threads, size_t dyn, hipStream_t s,
-                      const ApplyArgs &a) {
+                      const Args &a) {
   if (dyn > (64u << 10)) {
     static std::atomic<size_t> opted{0};  // per kernel instantiation
     if (opted.load(std::memory_order_relaxed) < dyn) {
@@ -87,6 +81,9 @@ inline int rows_bucket(uint32_t r) { return r <= 8 ? static_cast<int>(r) : 16; }
 bool vector_ok(const ApplyArgs &a);
 
 hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s);
+// One launch of per-stripe descriptors (DescArgs, rs_args.h): k <= kSlotK,
+// r <= kSlotR, 16-B aligned pointers and shares (the host checks).
+hipError_t launch_apply_desc(const DescArgs &a, hipStream_t s);
 
 // Bit-sliced encoders with the generator compiled in (rs_bitslice.hpp) for
 // the (k, n) Storb's large objects use. a.in / a.out hold the k data and

@@ -6,4 +6,7 @@ namespace storb_rs {
 hipError_t dispatch_perm_k8(const ApplyArgs &a, hipStream_t s) {
   return go_perm_r<8>(a, s);
 }
+hipError_t dispatch_desc_k8(const DescArgs &a, hipStream_t s) {
+  return go_desc_r<8>(a, s);
+}
 }  // namespace storb_rs

@@ -187,13 +187,6 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
   return STORB_RS_OK;
 }
 
-// STORB_RS_FUSED_ASSEMBLY=0: survivors are copied before the kernel instead
-// of by it (kept for the A/B measurement).
-static bool fused_assembly_on() {
-  const char *e = std::getenv("STORB_RS_FUSED_ASSEMBLY");
-  return e == nullptr || e[0] != '0';
-}
-
 // Whether the table kernel's COPY instantiations can do the assembly: they
 // exist for k <= kCopyMaxK in the dwordx4 register-table kernel (not the LDS
 // comparison variant), and every share base / stride must be 16-B aligned.
@@ -233,11 +226,6 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
           uint8_t *const *copy, const size_t *copy_stride) {
   if ((rows == 0 && !copy) || block == 0 || nstripes == 0) return STORB_RS_OK;
   int rc;
-  if (copy && !fused_assembly_on()) {
-    if ((rc = copy_first(ctx, k, d_in, in_stride, copy, copy_stride, block, nstripes, s))) return rc;
-    copy = nullptr;
-    if (rows == 0) return STORB_RS_OK;
-  }
   if (rows > 0 && ctx->variant == STORB_RS_KERNEL_AUTO && k <= static_cast<uint32_t>(kMaxIn) &&
       rows <= jit::kMaxRows &&
       jit::wanted(k, rows, static_cast<uint64_t>(k + rows) * block * nstripes)) {
@@ -538,6 +526,8 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto &e : ctx->desc_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto &sl : ctx->async_slots) {  // unfinished async ops: their work ends here
     (void)hipStreamSynchronize(sl->stream);
     (void)hipStreamDestroy(sl->stream);
@@ -708,45 +698,15 @@ int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t 
   if (data_stride == 0) data_stride = static_cast<size_t>(k) * block;
   if (parity_stride == 0) parity_stride = static_cast<size_t>(n - k) * block;
   if (out_stride == 0) out_stride = static_cast<size_t>(k) * block;
-  std::vector<uint32_t> slot_idx, slot_pos, missing;
-  int rc = select_shares(ctx, k, n, share_idx, nshares, slot_idx, slot_pos);
-  if (rc) return rc;
-  std::vector<uint8_t> coef;
-  rc = decode_rows(ctx, k, n, slot_idx, coef, missing);
+  trim_patterns(ctx);
+  const Pattern *p = nullptr;
+  std::vector<uint32_t> slot_pos;
+  const int rc = get_pattern(ctx, k, n, share_idx, nshares, &p, slot_pos);
   if (rc) return rc;
   if (block == 0 || nstripes == 0) return STORB_RS_OK;
   DeviceGuard g(ctx->device);
-  hipStream_t s = pick_stream(ctx, hip_stream);
-  std::vector<const uint8_t *> in(k);
-  std::vector<size_t> ins(k);
-  for (uint32_t c = 0; c < k; c++) {
-    const uint32_t id = slot_idx[c];
-    if (id < k) {
-      if (!d_data) return fail(ctx, STORB_RS_EINVAL, "survivor in null data region");
-      in[c] = d_data + static_cast<size_t>(id) * block;
-      ins[c] = data_stride;
-    } else {
-      if (!d_parity) return fail(ctx, STORB_RS_EINVAL, "survivor in null parity region");
-      in[c] = d_parity + static_cast<size_t>(id - k) * block;
-      ins[c] = parity_stride;
-    }
-  }
-  std::vector<uint8_t *> out(missing.size());
-  std::vector<size_t> outs(missing.size(), out_stride);
-  for (size_t r = 0; r < missing.size(); r++)
-    out[r] = d_out + static_cast<size_t>(missing[r]) * block;
-  // Surviving data shares: in place when d_out aliases d_data; else stored
-  // to their slots of d_out by the decode kernel itself as it reads them
-  // (fused assembly), or, where no such kernel applies, copied first (apply).
-  std::vector<uint8_t *> copy(k, nullptr);
-  std::vector<size_t> copys(k, out_stride);
-  const bool assemble = d_out != d_data || out_stride != data_stride;
-  if (assemble)
-    for (uint32_t c = 0; c < k; c++)
-      if (slot_idx[c] < k) copy[c] = d_out + static_cast<size_t>(c) * block;
-  return apply(ctx, k, static_cast<uint32_t>(missing.size()), coef.data(), in.data(), ins.data(),
-               out.data(), outs.data(), block, nstripes, s, assemble ? copy.data() : nullptr,
-               assemble ? copys.data() : nullptr);
+  return decode_pattern_batch(ctx, k, block, nstripes, *p, d_data, data_stride, d_parity,
+                              parity_stride, d_out, out_stride, pick_stream(ctx, hip_stream));
 }
 
 int storb_rs_repair_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,

@@ -28,6 +28,7 @@ between devices: each slice is host in / host out on its own GPU.
 """
 from __future__ import annotations
 
+import heapq
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -157,6 +158,50 @@ def encode_object(data, ctx: Optional[_lib.Context] = None,
                            for i in range(m)])
             shares.append(sh)
     return EncodedObject(chunks, pieces, shares)
+
+
+FETCH_THREADS = 10  # download.rs:28 THREAD_COUNT
+
+
+def download_arrivals(k: int, m: int, rng: np.random.Generator, fail=(), sigma: float = 0.5,
+                      threads: int = FETCH_THREADS) -> List[int]:
+    """The pieces of one chunk that produce_chunk collects, in arrival order
+    (download.rs:363-451), simulated: the m pieces are queued in piece_idx
+    order (:424-428, get_pieces_by_chunk is ORDER BY piece_idx); `threads`
+    workers each take the next queued piece when free (:378-383) and fetch it
+    in a lognormal(0, sigma) time; a piece whose miner is in `fail` yields
+    nothing (:403-405); the collector keeps pieces until more than k unique
+    ones are in hand (:434-451), i.e. the first k + 1 to arrive (all that
+    arrive, if fewer). decode_chunk then sorts them and uses the first k by
+    index (piece.rs:368-381) -- see download_survivors."""
+    fail = set(fail)
+    heap = []
+    nxt = 0
+    for _ in range(min(threads, m)):
+        heapq.heappush(heap, (float(rng.lognormal(0.0, sigma)), nxt))
+        nxt += 1
+    got: List[int] = []
+    while heap:
+        t, idx = heapq.heappop(heap)
+        if idx not in fail:
+            got.append(idx)
+        if nxt < m:  # the worker that finished takes the next queued piece
+            heapq.heappush(heap, (t + float(rng.lognormal(0.0, sigma)), nxt))
+            nxt += 1
+    collected: List[int] = []
+    for idx in got:
+        if len(collected) > k:  # `unique_pieces.len() > k` -> break (:443-447)
+            break
+        collected.append(idx)
+    return collected
+
+
+def download_survivors(k: int, m: int, rng: np.random.Generator, fail=(),
+                       sigma: float = 0.5) -> List[int]:
+    """The k shares decode_chunk hands to Fec::decode for one downloaded chunk
+    (first k by index of the pieces collected, piece.rs:368-381); fewer than k
+    means reconstruct_chunk's Err (piece.rs:462-473)."""
+    return sorted(download_arrivals(k, m, rng, fail, sigma))[:k]
 
 
 def reconstruct_object(chunks: Sequence[ChunkValue], fetched: Sequence[Dict[int, bytes]],

@@ -23,9 +23,8 @@ def test_bs_split_rule_is_the_one_mirrored():
     assert re.search(r"constexpr int kSplitGroup = 2;", src)
 
 
-def test_jit_blocks_match_row_split_and_row_blocks(monkeypatch):
+def test_jit_blocks_match_row_split_and_row_blocks():
     bench = load_bench()
-    monkeypatch.delenv("STORB_RS_JIT_SPLIT", raising=False)
     for k in (8, 12, 16, 17, 24, 40, 41, 63, 64):
         for rows in range(1, 33):
             if k % 2 == 0 and 16 < rows <= 32:
@@ -34,9 +33,7 @@ def test_jit_blocks_match_row_split_and_row_blocks(monkeypatch):
                 nb = -(-rows // 16)
                 want = (nb, rows // nb)
             assert bench.jit_blocks(k, rows) == want, (k, rows)
-    monkeypatch.setenv("STORB_RS_JIT_SPLIT", "0")
-    assert bench.jit_blocks(64, 32) == (2, 16)
-    assert bench.jit_blocks(64, 20) == (2, 10)
+    assert bench.jit_blocks(41, 20) == (2, 10)
 
 
 def test_line_extras_cpu_baseline_on_every_rank0_line():

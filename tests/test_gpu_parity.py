@@ -402,14 +402,14 @@ FUSED_CASES = [(4, 6, (0, 1)), (4, 6, ()), (4, 6, (4, 5)), (8, 12, (0, 3, 5)),
 
 @pytest.mark.parametrize("k,n,erased", FUSED_CASES)
 @pytest.mark.parametrize("B,ns", [(4096 * 2, 5), (4096 * 3 + 16 * 5, 3)])
-@pytest.mark.parametrize("mode", ["fused", "copy_first", "lds", "strided"])
+@pytest.mark.parametrize("mode", ["fused", "lds", "strided"])
 def test_dev_decode_separate_output_assembly(ctx, monkeypatch, k, n, erased, B, ns, mode):
     """decode_chunk returns a fresh chunk (piece.rs:363-387): decode into a
     separate buffer stores every surviving data share from the decode
     kernel's own loads (fused assembly, k <= 16) -- full tiles and a ragged
     last tile, nothing missing (pure assembly) and a strided output --
-    byte-identical to copying the survivors first (STORB_RS_FUSED_ASSEMBLY=0)
-    and to the LDS comparison variant, and every stripe equals the input."""
+    byte-identical to the LDS comparison variant (which copies the survivors
+    first), and every stripe equals the input."""
     host = rnd(ns * k * B, 7 * k + n + B + len(erased))
     data = to_dev(host)
     par = torch.zeros(ns * (n - k) * B, dtype=torch.uint8, device=DEV)
@@ -423,8 +423,6 @@ def test_dev_decode_separate_output_assembly(ctx, monkeypatch, k, n, erased, B, 
     pad = 3 * 16 if mode == "strided" else 0
     ostride = k * B + pad
     out = torch.full((ns * ostride,), 0x5A, dtype=torch.uint8, device=DEV)
-    if mode == "copy_first":
-        monkeypatch.setenv("STORB_RS_FUSED_ASSEMBLY", "0")
     if mode == "lds":
         ctx.set_kernel(_lib.KERNEL_LDS)
     try:
