@@ -306,6 +306,11 @@ int storb_rs_decode_async(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                           storb_rs_notify_fn notify, void *user, storb_rs_op **op);
 int storb_rs_op_test(const storb_rs_op *op);
 int storb_rs_op_finish(storb_rs_op *op);
+/* A notify function for the calls above that only wakes a waiter: writes an
+ * 8-byte 1 to the eventfd (or pipe) whose descriptor is user, cast from
+ * intptr_t. An event loop polls the descriptor (tokio AsyncFd, Python
+ * selectors) instead of running code on the HIP runtime thread. */
+void storb_rs_notify_fd(void *user);
 
 /* Synchronise the context's own streams and the HIP null stream of its
  * device (where device calls given hip_stream = NULL run). Work the caller

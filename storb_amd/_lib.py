@@ -16,6 +16,7 @@ import ctypes as C
 import os
 import subprocess
 import threading
+import weakref
 from typing import Optional, Sequence
 
 import numpy as np
@@ -122,6 +123,8 @@ def _declare(L):
                                         NOTIFY_FN, vp, C.POINTER(vp)]
     L.storb_rs_op_test.argtypes = [vp]
     L.storb_rs_op_finish.argtypes = [vp]
+    L.storb_rs_notify_fd.argtypes = [vp]
+    L.storb_rs_notify_fd.restype = None
     L.storb_rs_set_kernel.argtypes = [vp, C.c_int]
     L.storb_rs_sync.argtypes = [vp]
     L.storb_rs_jit_stats.argtypes = [C.POINTER(JitStats)]
@@ -359,11 +362,14 @@ class Context:
         op = AsyncOp(self, notify)
         rc = lib().storb_rs_encode_async(self._h, k, n, buf.ctypes.data if buf.size else None,
                                          buf.size, ptrs, C.byref(b), C.byref(pad), op._cb,
-                                         None, C.byref(op._h))
+                                         op._user, C.byref(op._h))
+        if rc != OK:
+            op._abandon()  # no op was created
         self._check(rc, "storb_rs_encode_async")
         op._keep = outs
         op._result = lambda: ([o[: b.value].tobytes() for o in outs], int(b.value),
                               int(pad.value))
+        op._started()
         return op
 
     def decode_async(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
@@ -376,10 +382,13 @@ class Context:
         out = np.zeros(max(outlen, 1), dtype=np.uint8)
         op = AsyncOp(self, notify)
         rc = lib().storb_rs_decode_async(self._h, k, n, ptrs, ids, len(arrs), block, padlen,
-                                         out.ctypes.data, op._cb, None, C.byref(op._h))
+                                         out.ctypes.data, op._cb, op._user, C.byref(op._h))
+        if rc != OK:
+            op._abandon()  # no op was created
         self._check(rc, "storb_rs_decode_async")
         op._keep = out
         op._result = lambda: out[:outlen].tobytes()
+        op._started()
         return op
 
     def repair(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
@@ -562,25 +571,137 @@ def encode_stripe_shares(share_idx: Sequence[Sequence[int]]):
 _tls = threading.local()
 
 
+class _Notifier:
+    """One daemon thread that runs the Python `notify` callables of async ops.
+
+    The C library wakes it without Python: an op's notify function is
+    storb_rs_notify_fd (a C function, never garbage-collected), which writes
+    to the op's eventfd from the HIP runtime thread. Nothing runs Python or
+    takes the GIL on that thread; this thread polls the eventfds and calls
+    the callables."""
+
+    def __init__(self):
+        import selectors
+        self._sel = selectors.DefaultSelector()
+        self._lock = threading.Lock()
+        self._wake = os.eventfd(0, os.EFD_NONBLOCK | os.EFD_CLOEXEC)
+        self._sel.register(self._wake, selectors.EVENT_READ, None)
+        self._pending = []
+        threading.Thread(target=self._run, name="storb_rs_notify", daemon=True).start()
+
+    def watch(self, fd: int, op: "AsyncOp"):
+        with self._lock:
+            self._pending.append((fd, op))
+        os.eventfd_write(self._wake, 1)
+
+    def _run(self):
+        import selectors
+        while True:
+            for key, _ in self._sel.select():
+                if key.data is None:
+                    try:
+                        os.eventfd_read(self._wake)
+                    except BlockingIOError:
+                        pass
+                    with self._lock:
+                        todo, self._pending = self._pending, []
+                    for fd, op in todo:
+                        self._sel.register(fd, selectors.EVENT_READ, op)
+                    continue
+                self._sel.unregister(key.fd)
+                os.close(key.fd)  # written once, by the op's notification
+                key.data._fd = None
+                key.data._fire()
+
+
+_notifier: Optional[_Notifier] = None
+_notifier_lock = threading.Lock()
+
+
+def _get_notifier() -> _Notifier:
+    global _notifier
+    with _notifier_lock:
+        if _notifier is None:
+            _notifier = _Notifier()
+        return _notifier
+
+
+class _OpState:
+    """What an AsyncOp's finalizer needs without the op: the C handle and
+    whether finish() ran (an op dropped unfinished is finished here, so its
+    staging slot is given back)."""
+
+    def __init__(self):
+        self.h = vp()
+        self.done = False
+
+    def finish_if_pending(self):
+        if not self.done and self.h:
+            self.done = True
+            lib().storb_rs_op_finish(self.h)
+
+
 class AsyncOp:
     """An in-flight storb_rs_*_async call: test() polls, finish() waits, writes
     the outputs and returns the call's result (exactly once). `notify` (a
-    Python callable, optional) runs once when the device work is done, on a
-    HIP runtime thread."""
+    Python callable, optional) runs once when the device work is done: on the
+    notifier thread (woken through an eventfd by storb_rs_notify_fd), or in
+    the calling thread when the op needed no device work; always before
+    finish() returns."""
 
     EAGAIN = 6
 
     def __init__(self, ctx: Context, notify=None):
         self._ctx = ctx  # keeps the context alive until finish
-        self._h = vp()
-        self._done = False
+        self._st = _OpState()
+        self._h = self._st.h
         self._keep = None
         self._result = None
         self._notify = notify
-        self._cb = NOTIFY_FN(lambda _u: notify()) if notify else C.cast(None, NOTIFY_FN)
+        self._fired = not notify
+        self._fire_lock = threading.Lock()
+        self._fd = None
+        if notify:
+            self._fd = os.eventfd(0, os.EFD_NONBLOCK | os.EFD_CLOEXEC)
+            fn = C.cast(lib().storb_rs_notify_fd, C.c_void_p).value
+            self._cb, self._user = NOTIFY_FN(fn), C.c_void_p(self._fd)
+        else:
+            self._cb, self._user = C.cast(None, NOTIFY_FN), None
+        self._fin = weakref.finalize(self, _OpState.finish_if_pending, self._st)
+
+    def _started(self):
+        """After the start call succeeded: hand the eventfd to the notifier
+        thread, or notify now if the op is already complete."""
+        if self._notify is None:
+            return
+        if self.test():  # done (the notification, queued before the event, has run)
+            os.close(self._fd)
+            self._fd = None
+            self._fire()
+        else:
+            _get_notifier().watch(self._fd, self)
+
+    def _abandon(self):
+        self._st.done = True
+        self._fin.detach()
+        if self._fd is not None:
+            os.close(self._fd)
+            self._fd = None
+
+    def _fire(self):
+        with self._fire_lock:
+            if self._fired:
+                return
+            self._fired = True
+        self._notify()
+
+    def fileno(self) -> int:
+        """The eventfd that becomes readable when the device work is done
+        (ops created with notify=...)."""
+        return -1 if self._fd is None else self._fd
 
     def test(self) -> bool:
-        if self._done:
+        if self._st.done:
             return True
         rc = lib().storb_rs_op_test(self._h)
         if rc == self.EAGAIN:
@@ -590,10 +711,13 @@ class AsyncOp:
         return True
 
     def finish(self):
-        if self._done:
+        if self._st.done:
             raise RuntimeError("op already finished")
-        self._done = True
+        self._st.done = True
         rc = lib().storb_rs_op_finish(self._h)
+        self._fin.detach()
+        if self._notify is not None:
+            self._fire()  # the stream is drained: the device work is done
         if rc != OK:
             raise StorbRsError(rc, "storb_rs_op_finish")
         return self._result()

@@ -57,6 +57,11 @@ struct PinBuf {
   ~PinBuf() {
     if (p) (void)hipHostFree(p);
   }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
     if (p) (void)hipHostFree(p);
@@ -82,7 +87,7 @@ struct Tables {
   uint8_t *dev = nullptr;
   size_t perm_bytes = 0;
   std::vector<size_t> b_off;
-  std::vector<uint8_t> host;      // upload source, kept until the table is evicted
+  std::vector<uint8_t> host;      // upload source, freed once the upload has completed
   hipStream_t home = nullptr;     // stream the upload was ordered on
   hipEvent_t uploaded = nullptr;  // recorded on `home` after the upload
   bool upload_done = false;
@@ -119,7 +124,9 @@ struct Pattern {
   uint64_t tick = 0;
 };
 
-constexpr int kDescRing = 4;  // page-locked descriptor upload buffers per context
+constexpr int kDescRing = 4;   // page-locked descriptor upload buffers per context
+constexpr int kDescForks = 2;  // extra streams the descriptor launches fan out to
+constexpr uint64_t kThreadsTable = 256;  // lanes (16-B columns) per table-kernel tile
 
 struct DeviceGuard {
   int prev = -1;
@@ -160,14 +167,18 @@ struct storb_rs_ctx {
   // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
   bool zc_batch = true;
   hipEvent_t slice_ev[storb_rs::detail::kMaxSlices] = {};  // sliced single-call pipeline
-  // Decode patterns by (k, n, slot share indices) and the page-locked ring
-  // the per-stripe descriptors are uploaded from (desc_ev[i]: that upload
-  // has been read by the device).
+  // Decode patterns by (k, n, slot share indices) and the ring the
+  // per-stripe descriptors go through: page-locked source, device copy;
+  // desc_ev[i]: the launches of that slot's last use have completed.
   std::map<std::vector<uint32_t>, std::unique_ptr<storb_rs::detail::Pattern>> patterns;
   uint64_t pattern_tick = 0;
   storb_rs::detail::PinBuf desc_pin[storb_rs::detail::kDescRing];
+  storb_rs::detail::DevBuf desc_dev[storb_rs::detail::kDescRing];
   hipEvent_t desc_ev[storb_rs::detail::kDescRing] = {};
   unsigned desc_next = 0;
+  hipStream_t fork[storb_rs::detail::kDescForks] = {};
+  hipEvent_t fork_ev[storb_rs::detail::kDescForks] = {};
+  hipEvent_t fork_start = nullptr;
   // Slots of the asynchronous host calls (host_async.cpp); async_mu guards
   // the busy flags, which finish() clears without holding mu.
   std::mutex async_mu;

@@ -6,10 +6,11 @@
 // survivor set, and with it the decode matrix, varies from chunk to chunk. A
 // launch per erasure pattern would be one small launch per chunk (and, with
 // the run-time-compiled kernels, one compile per pattern). Here a batch of
-// chunks is ONE launch per missing-row count: every workgroup reads its own
-// stripe's descriptor -- the k input pointers, the rebuilt rows' pointers,
-// the assembly targets -- and its own pattern's v_perm tables
-// (rs_device.hpp rs_apply_desc; the table kernel's tile, unchanged).
+// chunks is one launch per missing-row count, the launches concurrent on
+// up to three streams: every workgroup reads its own stripe's descriptor --
+// the k input pointers, the rebuilt rows' pointers, the assembly targets --
+// and its own pattern's v_perm tables (rs_device.hpp rs_apply_desc; the
+// table kernel's tile, unchanged).
 //
 // Patterns (slot arrangement, inverted rows, tables) are cached per context.
 #include <hip/hip_runtime_api.h>
@@ -80,86 +81,116 @@ bool desc_ok(const storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block) {
          std::min(k, n - k) <= static_cast<uint32_t>(kSlotR) && block % kAlign == 0;
 }
 
+// Tiles per workgroup of a descriptor launch set covering `tiles` tiles in
+// all: enough workgroups to fill the chip several times over, else amortise
+// each workgroup's record -> tables -> loads start-up over several tiles.
+uint32_t desc_tpw(uint64_t tiles) {
+  return static_cast<uint32_t>(std::min<uint64_t>(8, std::max<uint64_t>(1, tiles / 8192)));
+}
+
 int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
                const std::vector<const Pattern *> &pats, const std::vector<uint64_t> &ptr,
                hipStream_t s) {
   const size_t W = 2 * static_cast<size_t>(k) + kSlotR;
-  std::vector<std::vector<uint32_t>> by_e(kSlotR + 1);
-  for (uint32_t i = 0; i < pats.size(); i++) {
-    const size_t e = pats[i]->missing.size();
-    if (e > static_cast<size_t>(kSlotR)) return fail(ctx, STORB_RS_EINVAL, "apply_desc: > 16 rows");
-    if (e || copy) by_e[e].push_back(i);
-  }
+  // One launch per rebuilt-row count, the launches spread over the caller's
+  // stream and two fork streams so they run concurrently: no launch waits
+  // out another's tail, and a small group (the few chunks that lost many
+  // shares) overlaps the big ones.
   struct Group {
-    uint32_t e, rb, rec_q, nitems;
-    size_t tab_off, rec_off;
-    std::vector<const Pattern *> distinct;
+    uint32_t r = 0, rec_q = 0;
+    std::vector<uint32_t> items;
+    size_t tab_off = 0, rec_off = 0, ntab = 0;
+    std::unordered_map<const Pattern *, size_t> tab_at;  // pattern -> its tables (PermTabs)
   };
-  std::vector<Group> groups;
-  size_t total = 0;
-  std::vector<uint32_t> local(pats.size());
-  for (uint32_t e = 0; e <= static_cast<uint32_t>(kSlotR); e++) {
-    if (by_e[e].empty()) continue;
-    Group g{};
-    g.e = e;
-    g.rb = static_cast<uint32_t>(rows_bucket(e ? e : 1));
-    g.rec_q = 1 + k + e + (copy ? k : 0);
-    g.nitems = static_cast<uint32_t>(by_e[e].size());
-    std::unordered_map<const Pattern *, uint32_t> seen;
-    for (uint32_t i : by_e[e]) {
-      auto f = seen.emplace(pats[i], static_cast<uint32_t>(g.distinct.size()));
-      if (f.second) g.distinct.push_back(pats[i]);
-      local[i] = f.first->second;
-    }
-    g.tab_off = total;
-    total = round_up(total + g.distinct.size() * k * g.rb * sizeof(PermTab), 256);
-    g.rec_off = total;
-    total = round_up(total + static_cast<size_t>(g.nitems) * g.rec_q * 8, 256);
-    groups.push_back(std::move(g));
+  std::vector<Group> by_r(kSlotR + 1);
+  for (uint32_t i = 0; i < pats.size(); i++) {
+    const uint32_t e = static_cast<uint32_t>(pats[i]->missing.size());
+    if (e > static_cast<uint32_t>(kSlotR)) return fail(ctx, STORB_RS_EINVAL, "apply_desc: > 16 rows");
+    if (e || copy) by_r[e].items.push_back(i);
   }
+  std::vector<Group *> groups;
+  for (uint32_t e = 0; e <= static_cast<uint32_t>(kSlotR); e++)
+    if (!by_r[e].items.empty()) {
+      by_r[e].r = e;
+      groups.push_back(&by_r[e]);
+    }
   if (groups.empty()) return STORB_RS_OK;
-  // Page-locked upload slot: reusable once its previous upload was read.
+  std::stable_sort(groups.begin(), groups.end(), [](const Group *a, const Group *b) {
+    return a->items.size() > b->items.size();
+  });
+  size_t total = 0;
+  uint64_t tiles = 0;
+  const uint64_t tps = (block / 16 + kThreadsTable - 1) / kThreadsTable;
+  for (Group *g : groups) {
+    g->rec_q = 1 + k + g->r + (copy ? k : 0);
+    g->tab_off = total;
+    for (uint32_t i : g->items)
+      if (g->tab_at.emplace(pats[i], g->ntab).second) g->ntab += pats[i]->tabs.size();
+    total = round_up(total + g->ntab * sizeof(PermTab), 256);
+    g->rec_off = total;
+    total = round_up(total + g->items.size() * g->rec_q * 8, 256);
+    tiles += tps * g->items.size();
+  }
+  const uint32_t tpw = desc_tpw(tiles);
+  // Upload slot (page-locked source + device copy), reusable once the
+  // launches of its previous use have completed.
   const unsigned slot = ctx->desc_next++ % kDescRing;
   if (ctx->desc_ev[slot]) HIP_TRY(ctx, hipEventSynchronize(ctx->desc_ev[slot]));
   else HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_ev[slot], hipEventDisableTiming));
   HIP_TRY(ctx, ctx->desc_pin[slot].ensure(total));
+  HIP_TRY(ctx, ctx->desc_dev[slot].ensure(total));
   uint8_t *h = ctx->desc_pin[slot].p;
-  for (const Group &g : groups) {
-    PermTab *t = reinterpret_cast<PermTab *>(h + g.tab_off);
-    for (size_t d = 0; d < g.distinct.size(); d++)
-      std::memcpy(t + d * k * g.rb, g.distinct[d]->tabs.data(),
-                  static_cast<size_t>(k) * g.rb * sizeof(PermTab));
-    uint64_t *rec = reinterpret_cast<uint64_t *>(h + g.rec_off);
-    for (uint32_t i : by_e[g.e]) {
+  for (Group *g : groups) {
+    PermTab *t = reinterpret_cast<PermTab *>(h + g->tab_off);
+    for (auto &pt : g->tab_at)
+      std::memcpy(t + pt.second, pt.first->tabs.data(), pt.first->tabs.size() * sizeof(PermTab));
+    uint64_t *rec = reinterpret_cast<uint64_t *>(h + g->rec_off);
+    for (uint32_t i : g->items) {
       const uint64_t *src = &ptr[i * W];
-      rec[0] = local[i];
+      rec[0] = static_cast<uint64_t>(g->tab_at[pats[i]]);
       std::memcpy(rec + 1, src, static_cast<size_t>(k) * 8);
-      std::memcpy(rec + 1 + k, src + k, static_cast<size_t>(g.e) * 8);
-      if (copy) std::memcpy(rec + 1 + k + g.e, src + k + kSlotR, static_cast<size_t>(k) * 8);
-      rec += g.rec_q;
+      std::memcpy(rec + 1 + k, src + k, static_cast<size_t>(g->r) * 8);
+      if (copy) std::memcpy(rec + 1 + k + g->r, src + k + kSlotR, static_cast<size_t>(k) * 8);
+      rec += g->rec_q;
     }
   }
-  uint8_t *dev = nullptr;
-  HIP_TRY(ctx, hipMallocAsync(reinterpret_cast<void **>(&dev), total, s));
+  const int nfork = static_cast<int>(std::min<size_t>(groups.size() - 1, kDescForks));
+  for (int f = 0; f < nfork; f++)
+    if (!ctx->fork[f]) {
+      HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->fork[f], hipStreamNonBlocking));
+      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->fork_ev[f], hipEventDisableTiming));
+    }
+  if (!ctx->fork_start && nfork)
+    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->fork_start, hipEventDisableTiming));
+  uint8_t *dev = ctx->desc_dev[slot].p;
   hipError_t e = hipMemcpyAsync(dev, h, total, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipEventRecord(ctx->desc_ev[slot], s);
+  if (e == hipSuccess && nfork) e = hipEventRecord(ctx->fork_start, s);
+  for (int f = 0; e == hipSuccess && f < nfork; f++) e = hipStreamWaitEvent(ctx->fork[f], ctx->fork_start, 0);
   for (size_t gi = 0; e == hipSuccess && gi < groups.size(); gi++) {
-    const Group &g = groups[gi];
+    const Group &g = *groups[gi];
     DescArgs a{};
     a.desc = reinterpret_cast<const uint64_t *>(dev + g.rec_off);
     a.ptab = reinterpret_cast<const PermTab *>(dev + g.tab_off);
     a.block = block;
     a.k = k;
-    a.r = g.e;
-    a.tab_rows = g.rb;
-    a.nitems = g.nitems;
+    a.r = g.r;
+    a.tpw = tpw;
+    a.nitems = static_cast<uint32_t>(g.items.size());
     a.copy = copy ? 1u : 0u;
     a.rec_qwords = g.rec_q;
-    e = launch_apply_desc(a, s);
+    const int lane = static_cast<int>(gi % (nfork + 1));  // 0 = the caller's stream
+    e = launch_apply_desc(a, lane ? ctx->fork[lane - 1] : s);
   }
-  const hipError_t ef = hipFreeAsync(dev, s);  // ordered after the launches
+  // join (also after a failed launch: earlier ones may be queued), then the
+  // slot's reuse event on the caller's stream
+  for (int f = 0; f < nfork; f++) {
+    const hipError_t r1 = hipEventRecord(ctx->fork_ev[f], ctx->fork[f]);
+    const hipError_t r2 = r1 == hipSuccess ? hipStreamWaitEvent(s, ctx->fork_ev[f], 0) : r1;
+    if (e == hipSuccess) e = r2;
+  }
+  const hipError_t er = hipEventRecord(ctx->desc_ev[slot], s);
   if (e != hipSuccess) return hip_fail(ctx, e, "apply_desc");
-  if (ef != hipSuccess) return hip_fail(ctx, ef, "hipFreeAsync(descriptors)");
+  if (er != hipSuccess) return hip_fail(ctx, er, "hipEventRecord(descriptors)");
   return STORB_RS_OK;
 }
 

@@ -20,6 +20,9 @@
 // finished op's slot is reused. The math is the synchronous calls' own
 // (encode_apply / apply, host_calls.cpp), so the bytes are identical.
 #include <hip/hip_runtime_api.h>
+#include <unistd.h>
+
+#include <cerrno>
 
 #include <algorithm>
 #include <cstring>
@@ -56,9 +59,17 @@ struct storb_rs_op {
 
 namespace {
 
+// The notification runs on a HIP runtime thread and owns its own copy of
+// (notify, user): nothing it reads depends on *op, which finish() deletes.
+struct Notify {
+  storb_rs_notify_fn fn;
+  void *user;
+};
+
 void notify_host_fn(void *p) {
-  storb_rs_op *op = static_cast<storb_rs_op *>(p);
-  op->notify(op->user);
+  Notify *n = static_cast<Notify *>(p);
+  n->fn(n->user);
+  delete n;
 }
 
 // A free slot of the context (created on demand, at most kMaxAsyncSlots).
@@ -85,15 +96,30 @@ int acquire_slot(storb_rs_ctx *ctx, AsyncSlot **out) {
   return STORB_RS_OK;
 }
 
+// A slot keeps its page-locked staging for the next op up to this size;
+// larger buffers (a 128-256 MiB k = 64 chunk) are released when the op is
+// finished, so idle slots never pin more than 64 x 2 x kSlotKeep bytes.
+constexpr size_t kSlotKeep = 32u << 20;
+
 void release_slot(storb_rs_ctx *ctx, AsyncSlot *s) {
+  if (s->in.cap > kSlotKeep) s->in.release();
+  if (s->out.cap > kSlotKeep) s->out.release();
   std::lock_guard<std::mutex> lk(ctx->async_mu);
   s->busy = false;
 }
 
-// Record completion on the slot's stream and queue the notification.
+// Queue the notification, then record completion on the slot's stream: an
+// op that tests done has had its notification delivered.
 int queue_completion(storb_rs_ctx *ctx, storb_rs_op *op) {
+  if (op->notify) {
+    Notify *n = new Notify{op->notify, op->user};
+    const hipError_t e = hipLaunchHostFunc(op->slot->stream, notify_host_fn, n);
+    if (e != hipSuccess) {
+      delete n;
+      return hip_fail(ctx, e, "hipLaunchHostFunc(notify)");
+    }
+  }
   HIP_TRY(ctx, hipEventRecord(op->slot->done, op->slot->stream));
-  if (op->notify) HIP_TRY(ctx, hipLaunchHostFunc(op->slot->stream, notify_host_fn, op));
   return STORB_RS_OK;
 }
 
@@ -307,8 +333,7 @@ int storb_rs_op_finish(storb_rs_op *op) {
   if (op->slot) {
     storb_rs_ctx *ctx = op->ctx;
     DeviceGuard g(ctx->device);
-    // The stream, not just the event: it also orders the notify host
-    // function, which reads *op.
+    // The stream: the kernel, the notification and the completion event.
     const hipError_t e = hipStreamSynchronize(op->slot->stream);
     if (e != hipSuccess) {
       rc = STORB_RS_EDEVICE;
@@ -331,6 +356,17 @@ int storb_rs_op_finish(storb_rs_op *op) {
   }
   delete op;
   return rc;
+}
+
+// Ready-made notify function: wakes a waiter blocked on (or polling) the
+// eventfd / pipe `(int)(intptr_t)user` by writing an 8-byte 1 to it.
+void storb_rs_notify_fd(void *user) {
+  const uint64_t one = 1;
+  const int fd = static_cast<int>(reinterpret_cast<intptr_t>(user));
+  ssize_t r;
+  do {
+    r = write(fd, &one, sizeof(one));
+  } while (r < 0 && errno == EINTR);
 }
 
 }  // extern "C"

@@ -29,7 +29,7 @@ struct CopySeg {
 
 class HostPool {
  public:
-  explicit HostPool(int nthreads) {
+  explicit HostPool(int nthreads, int spin_us = 60) : spin_us_(spin_us) {
     for (int i = 1; i < nthreads; i++) workers_.emplace_back([this] { loop(); });
   }
   ~HostPool() {
@@ -47,7 +47,7 @@ class HostPool {
   int size() const { return static_cast<int>(workers_.size()) + 1; }
 
   // f(i) for every i in [0, parts); the caller takes part too. Blocking.
-  // Workers that finished a job spin for kSpinUs before sleeping, so the
+  // Workers that finished a job spin for spin_us before sleeping, so the
   // back-to-back jobs of one call (pack, launch, unpack of each slice) start
   // without a futex wake-up each (~5-20 us on a busy host).
   void run(int parts, const std::function<void(int)> &f) {
@@ -74,20 +74,30 @@ class HostPool {
     job_ = nullptr;
   }
 
-  // memcpy split into >= 1 MiB slices over the pool.
+  // memcpy split over the pool (copy_segs' rule).
   void copy(void *dst, const void *src, size_t bytes) {
     CopySeg s{static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), bytes};
-    copy_segs(&s, 1, 1u << 20);
+    copy_segs(&s, 1);
   }
 
-  // Copy / zero-fill a list of byte ranges, the total split evenly over up
-  // to size() threads with at least min_part bytes each.
-  void copy_segs(const CopySeg *segs, size_t nsegs, size_t min_part = 64u << 10) {
+  // How many threads a copy of `total` bytes into page-locked memory takes.
+  // Measured (tools/poolbench.cpp, profiles/r3_poolbench.txt, GPU-box host):
+  // one thread copies 256 KiB in 1.7 us and 1 MiB in 21 us; two threads 1 MiB
+  // in 5.2 us, while 4 or 8 (waking, claiming parts) took 13-20 us; from
+  // 4 MiB on 8 threads win (28-35 us against 44 for two, 84 for one).
+  int parts_for(size_t total) const {
+    if (total < (384u << 10)) return 1;
+    if (total < (4u << 20)) return std::min(2, size());
+    return static_cast<int>(std::max<size_t>(2, std::min<size_t>(size(), total / (512u << 10))));
+  }
+
+  // Copy / zero-fill a list of byte ranges, the total split evenly over
+  // parts_for(total) threads.
+  void copy_segs(const CopySeg *segs, size_t nsegs) {
     size_t total = 0;
     for (size_t i = 0; i < nsegs; i++) total += segs[i].len;
     if (total == 0) return;
-    const int parts = static_cast<int>(
-        std::max<size_t>(1, std::min<size_t>(size(), total / std::max<size_t>(min_part, 1))));
+    const int parts = parts_for(total);
     const size_t per = ((total + parts - 1) / parts + 63) & ~static_cast<size_t>(63);
     run(parts, [&](int p) {
       size_t lo = std::min(total, static_cast<size_t>(p) * per), hi = std::min(total, lo + per);
@@ -106,7 +116,7 @@ class HostPool {
   }
 
  private:
-  static constexpr int kSpinUs = 60;
+  const int spin_us_;  // how long a worker spins for the next job before sleeping
 
   void work() {
     for (;;) {
@@ -132,7 +142,7 @@ class HostPool {
         __builtin_ia32_pause();
 #endif
         if ((spin & 255) == 0 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs))
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_))
           break;
       }
       {

@@ -63,18 +63,21 @@ struct ApplyArgs {
 // shares (Storb's download keeps whichever k + 1 pieces arrive first,
 // download.rs:363-451, so the survivor set varies from chunk to chunk). Item
 // i of the launch is the record desc + i * rec_qwords (8-byte words):
-//   [0]                  pattern t: its tables at ptab + t * k * tab_rows
+//   [0]                  offset (in PermTabs) of the item's tables in ptab,
+//                        [input][rows_bucket(r)]
 //   [1 .. k]             input pointers, slot order
 //   [k+1 .. k+r]         output row pointers
 //   [k+r+1 .. 2k+r]      (copy != 0) where input j is also stored, 0 = nowhere
-// Every item of a launch rebuilds r rows with its own matrix and pointers;
-// the stripes (and shares) of different items need not be related at all.
+// Every item rebuilds r rows with its own matrix and pointers; the stripes
+// (and shares) of different items need not be related at all. A workgroup
+// covers tpw consecutive tiles of one item.
 struct DescArgs {
   const uint64_t *desc;
   const PermTab *ptab;
   uint64_t block;  // bytes per share
-  uint32_t k, r;
-  uint32_t tab_rows;  // = rows_bucket(r ? r : 1)
+  uint32_t k;
+  uint32_t r;
+  uint32_t tpw;    // tiles per workgroup
   uint32_t nitems;
   uint32_t copy;
   uint32_t rec_qwords;  // 1 + k + r (+ k with copy)

@@ -141,16 +141,16 @@ struct ArgsView {
 
 struct DescView {
   const uint64_t *rec;  // this item's record (wave-uniform: scalar loads)
-  uint32_t k, r;
+  uint32_t k, ro;       // ro = output slots per record
   __device__ __forceinline__ const uint8_t *in(int j) const {
     return reinterpret_cast<const uint8_t *>(rec[1 + j]);
   }
   __device__ __forceinline__ uint8_t *out(int i) const {
     return reinterpret_cast<uint8_t *>(rec[1 + k + i]);
   }
-  __device__ __forceinline__ bool has_copy(int j) const { return rec[1 + k + r + j] != 0; }
+  __device__ __forceinline__ bool has_copy(int j) const { return rec[1 + k + ro + j] != 0; }
   __device__ __forceinline__ uint8_t *copy(int j) const {
-    return reinterpret_cast<uint8_t *>(rec[1 + k + r + j]);
+    return reinterpret_cast<uint8_t *>(rec[1 + k + ro + j]);
   }
   __device__ __forceinline__ bool accumulate() const { return false; }
 };
@@ -346,20 +346,25 @@ __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
                                                      base + threadIdx.x);
 }
 
-// The same tile for a launch of per-stripe descriptors (DescArgs): item
-// blockIdx / tiles-per-share reads its record -- the inputs, outputs and
-// assembly targets of its own stripe and the tables of its own matrix --
-// with scalar loads, then runs perm_tile exactly as rs_apply_perm does.
+// The same tile for a launch of per-stripe descriptors (DescArgs). A
+// workgroup reads its item's record -- the inputs, outputs and assembly
+// targets of its own stripe, the offset of its own matrix's tables -- with
+// scalar loads, stages the tables in LDS, then runs perm_tile exactly as
+// rs_apply_perm does over `tpw` consecutive tiles of the stripe: the record
+// -> tables -> first loads chain (~1-2 us of dependent latency a workgroup
+// of one tile pays before its first byte streams) is paid once per tpw tiles.
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false,
           bool COPY = false>
 __global__ __launch_bounds__(T) void rs_apply_desc(const DescArgs a) {
   constexpr uint32_t TILE = T * U;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + TILE - 1) / TILE;
-  const uint32_t item = blockIdx.x / tps;
-  const uint32_t base = (blockIdx.x - item * tps) * TILE;
+  const uint32_t wps = (tps + a.tpw - 1) / a.tpw;  // workgroups per stripe
+  const uint32_t item = blockIdx.x / wps;
+  const uint32_t t0 = (blockIdx.x - item * wps) * a.tpw;
+  const uint32_t t1 = t0 + a.tpw < tps ? t0 + a.tpw : tps;
   const uint64_t *rec = a.desc + static_cast<uint64_t>(item) * a.rec_qwords;
-  const PermTab *tabs = a.ptab + static_cast<uint64_t>(rec[0] & 0xFFFFFFFFu) * a.k * RM;
+  const PermTab *tabs = a.ptab + (rec[0] & 0xFFFFFFFFu);
   if constexpr (TL) {
     __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * RM];
     const uint32_t n16 = (COPY && a.r == 0) ? 0u : a.k * RM * (sizeof(PermTab) / 16);
@@ -369,12 +374,15 @@ __global__ __launch_bounds__(T) void rs_apply_desc(const DescArgs a) {
     tabs = lds_ptab;
   }
   const DescView v{rec, a.k, a.r};
-  if (base + TILE <= cols)
-    perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, a.r, cols,
-                                                      base + threadIdx.x);
-  else
-    perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, a.r, cols,
-                                                     base + threadIdx.x);
+  for (uint32_t t = t0; t < t1; t++) {
+    const uint32_t base = t * TILE;
+    if (base + TILE <= cols)
+      perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, a.r, cols,
+                                                        base + threadIdx.x);
+    else
+      perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, a.r, cols,
+                                                       base + threadIdx.x);
+  }
 }
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
@@ -398,7 +406,9 @@ hipError_t launch_perm(const ApplyArgs &a, hipStream_t s, int occ = 0, int occ_c
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
 hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_copy = 0) {
   const uint64_t cols = a.block >> 4;
-  const uint64_t blocks = ((cols + T * U - 1) / (T * U)) * a.nitems;
+  const uint64_t tps = (cols + T * U - 1) / (T * U);
+  if (a.tpw == 0) return hipErrorInvalidValue;
+  const uint64_t blocks = ((tps + a.tpw - 1) / a.tpw) * a.nitems;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
   const size_t dyn = cap_lds(wg_cap(a.copy ? occ_copy : occ),

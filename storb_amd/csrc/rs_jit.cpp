@@ -16,8 +16,7 @@
 // a compile); at most STORB_RS_JIT_MAX kernels (default 256) are loaded, the
 // least recently used one unloaded for a new one once every launch of it
 // has completed (per-stream launch events), so no queued launch can outlive
-// its code object. One compile thread, at a lower CPU priority than the
-// host copy workers it shares the CPUs with.
+// its code object. One compile thread.
 #include <hip/hip_runtime_api.h>
 #include <hip/hiprtc.h>
 
@@ -36,9 +35,6 @@
 #include <unordered_map>
 #include <vector>
 
-#include <sys/resource.h>
-#include <sys/syscall.h>
-#include <unistd.h>
 
 #include "../../include/storb_rs.h"
 #include "gf256.hpp"
@@ -267,9 +263,9 @@ class Jit {
   }
 
   void run() {
-    // Below the host copy workers (same CPUs, cgroup quota): a compile must
-    // not slow the copies of the calls running meanwhile on the table kernel.
-    (void)setpriority(PRIO_PROCESS, static_cast<id_t>(syscall(SYS_gettid)), 10);
+    // (A nice-10 compile thread starved on the GPU box: 0 of 32 queued
+    // compiles done after 4 s of decode calls, tools/jit_fuzz.py,
+    // profiles/r3_jit_fuzz_nice10.jsonl. One thread at normal priority.)
     for (;;) {
       std::shared_ptr<Entry> e;
       {

@@ -115,8 +115,7 @@ hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s) {
 
 hipError_t launch_apply_desc(const DescArgs &a, hipStream_t s) {
   if (a.k == 0 || a.k > kSlotK || a.r > kSlotR || (a.copy && a.k > kCopyMaxK) ||
-      (a.r == 0 && !a.copy) || a.block % 16 ||
-      a.tab_rows != static_cast<uint32_t>(rows_bucket(a.r ? a.r : 1)) ||
+      (a.r == 0 && !a.copy) || a.block % 16 || a.tpw == 0 ||
       a.rec_qwords != 1 + a.k + a.r + (a.copy ? a.k : 0))
     return hipErrorInvalidValue;
   if (a.block == 0 || a.nitems == 0) return hipSuccess;

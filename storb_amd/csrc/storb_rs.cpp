@@ -95,15 +95,18 @@ static int evict_tables(storb_rs_ctx *ctx) {
 
 // Make t usable on stream s: a stream other than the upload's waits for it
 // on the device (once the upload is known complete, no wait is issued).
+// Once the upload is known complete the host copy is dropped (a k = 64 x
+// 32-row matrix is ~130 KiB of tables).
 static int tables_ready(storb_rs_ctx *ctx, Tables *t, hipStream_t s) {
-  if (t->upload_done || s == t->home) return STORB_RS_OK;
+  if (t->upload_done) return STORB_RS_OK;
   const hipError_t q = hipEventQuery(t->uploaded);
   if (q == hipSuccess) {
     t->upload_done = true;
+    std::vector<uint8_t>().swap(t->host);
     return STORB_RS_OK;
   }
   if (q != hipErrorNotReady) return hip_fail(ctx, q, "hipEventQuery(tables)");
-  HIP_TRY(ctx, hipStreamWaitEvent(s, t->uploaded, 0));
+  if (s != t->home) HIP_TRY(ctx, hipStreamWaitEvent(s, t->uploaded, 0));
   return STORB_RS_OK;
 }
 
@@ -526,8 +529,19 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto &e : ctx->desc_ev)
-    if (e) (void)hipEventDestroy(e);
+  for (int f = 0; f < kDescForks; f++) {
+    if (ctx->fork[f]) {
+      (void)hipStreamSynchronize(ctx->fork[f]);
+      (void)hipStreamDestroy(ctx->fork[f]);
+    }
+    if (ctx->fork_ev[f]) (void)hipEventDestroy(ctx->fork_ev[f]);
+  }
+  if (ctx->fork_start) (void)hipEventDestroy(ctx->fork_start);
+  for (auto &e : ctx->desc_ev)  // descriptor launches may run on callers' streams
+    if (e) {
+      (void)hipEventSynchronize(e);
+      (void)hipEventDestroy(e);
+    }
   for (auto &sl : ctx->async_slots) {  // unfinished async ops: their work ends here
     (void)hipStreamSynchronize(sl->stream);
     (void)hipStreamDestroy(sl->stream);

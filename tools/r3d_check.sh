@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 3: mixed-row descriptor decode, async notify rewrite, JIT eviction
+# and churn fuzz, host copy pool, per-call latency.
+set -uo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r3d; mkdir -p $O
+timeout -k 10 120 ./tools/_build/poolbench > $O/poolbench.txt 2>&1 || { echo "poolbench failed"; tail $O/poolbench.txt; exit 1; }
+echo poolbench done
+for th in 8 1; do
+  STORB_RS_HOST_THREADS=$th timeout -k 10 120 ./tools/_build/callbench 41 > $O/callbench_threads$th.jsonl 2>&1 || { echo "callbench failed"; tail $O/callbench_threads$th.jsonl; exit 1; }
+done
+echo callbench done
+timeout -k 10 500 python -u -m pytest tests/test_gpu_patterns.py tests/test_gpu_async.py tests/test_gpu_jit.py tests/test_rust_binding.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for cfg in "5" "6" "2"; do
+  timeout -k 10 300 python -u bench.py --config $cfg --erase-pattern download --no-traffic --cpu-seconds 0 --no-host-path > $O/bench_c${cfg}_download.json 2> $O/bench_c${cfg}_download.err || { echo "bench c$cfg failed"; tail -20 $O/bench_c${cfg}_download.err; exit 1; }
+  python - $O/bench_c${cfg}_download.json <<'PY'
+import json,sys
+d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+r=d["roofline"]
+print(d["config"]["baseline_config"], d["value"], r["frac"], r["leg_ms"], d["config"]["patterns"]["lost_data_shares_histogram"])
+PY
+done
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c5_download -o run -- python3 bench.py --config 5 --erase-pattern download --no-host-path --no-traffic --cpu-seconds 0 --minimal > $O/trace_c5_download.log 2>&1 || { echo "trace failed"; tail -20 $O/trace_c5_download.log; exit 1; }
+echo traced
+STORB_RS_JIT_MAX=32 timeout -k 10 400 python -u tools/jit_fuzz.py 10000 2000 > $O/jit_fuzz.jsonl 2>&1 || { echo "fuzz failed"; tail -5 $O/jit_fuzz.jsonl; exit 1; }
+tail -1 $O/jit_fuzz.jsonl
