@@ -674,12 +674,15 @@ class AsyncOp:
         thread, or notify now if the op is already complete."""
         if self._notify is None:
             return
-        if self.test():  # done (the notification, queued before the event, has run)
-            os.close(self._fd)
-            self._fd = None
+        # The eventfd is closed only by the notifier thread, once the
+        # notification's write has arrived: closing it here when the op
+        # already tests done would let a notification that runs after the
+        # completion event (nothing in HIP's contract orders a host function
+        # before a later event on the stream) write into a closed descriptor
+        # whose number the process may have reused.
+        if self.test():
             self._fire()
-        else:
-            _get_notifier().watch(self._fd, self)
+        _get_notifier().watch(self._fd, self)
 
     def _abandon(self):
         self._st.done = True

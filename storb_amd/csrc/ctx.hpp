@@ -125,7 +125,6 @@ struct Pattern {
 };
 
 constexpr int kDescRing = 4;   // page-locked descriptor upload buffers per context
-constexpr int kDescForks = 2;  // extra streams the descriptor launches fan out to
 constexpr uint64_t kThreadsTable = 256;  // lanes (16-B columns) per table-kernel tile
 
 struct DeviceGuard {
@@ -167,6 +166,11 @@ struct storb_rs_ctx {
   // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
   bool zc_batch = true;
   hipEvent_t slice_ev[storb_rs::detail::kMaxSlices] = {};  // sliced single-call pipeline
+  // Slice-completion words the single-call streams write (64 B apart) and
+  // the host spins on (host_calls.cpp slice_signal / slice_wait).
+  storb_rs::detail::PinBuf flag_pin;
+  uint8_t *flag_dev = nullptr;
+  uint32_t flag_seq = 0;
   // Decode patterns by (k, n, slot share indices) and the ring the
   // per-stripe descriptors go through: page-locked source, device copy;
   // desc_ev[i]: the launches of that slot's last use have completed.
@@ -176,9 +180,6 @@ struct storb_rs_ctx {
   storb_rs::detail::DevBuf desc_dev[storb_rs::detail::kDescRing];
   hipEvent_t desc_ev[storb_rs::detail::kDescRing] = {};
   unsigned desc_next = 0;
-  hipStream_t fork[storb_rs::detail::kDescForks] = {};
-  hipEvent_t fork_ev[storb_rs::detail::kDescForks] = {};
-  hipEvent_t fork_start = nullptr;
   // Slots of the asynchronous host calls (host_async.cpp); async_mu guards
   // the busy flags, which finish() clears without holding mu.
   std::mutex async_mu;

@@ -6,8 +6,8 @@
 // survivor set, and with it the decode matrix, varies from chunk to chunk. A
 // launch per erasure pattern would be one small launch per chunk (and, with
 // the run-time-compiled kernels, one compile per pattern). Here a batch of
-// chunks is one launch per missing-row count, the launches concurrent on
-// up to three streams: every workgroup reads its own stripe's descriptor --
+// chunks is one launch (rows 0-4, the common case) plus one per larger
+// missing-row count: every workgroup reads its own stripe's descriptor --
 // the k input pointers, the rebuilt rows' pointers, the assembly targets --
 // and its own pattern's v_perm tables (rs_device.hpp rs_apply_desc; the
 // table kernel's tile, unchanged).
@@ -82,42 +82,49 @@ bool desc_ok(const storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block) {
 }
 
 // Tiles per workgroup of a descriptor launch set covering `tiles` tiles in
-// all: enough workgroups to fill the chip several times over, else amortise
-// each workgroup's record -> tables -> loads start-up over several tiles.
+// all. One: two or more per workgroup measured slower at every size once the
+// records are scalar loads (k = 16 download mix: tpw 1 / 2 / 4 / 8 = 66.8 /
+// 63.3 / 55.0 / 54.0 % per-row-count, 72.4 / 65.2 % mixed, descbench); more
+// only when the grid would exceed the launch limit.
 uint32_t desc_tpw(uint64_t tiles) {
-  return static_cast<uint32_t>(std::min<uint64_t>(8, std::max<uint64_t>(1, tiles / 8192)));
+  return static_cast<uint32_t>(std::max<uint64_t>(1, (tiles + 0x3FFFFFFFull) / 0x40000000ull));
 }
 
 int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
                const std::vector<const Pattern *> &pats, const std::vector<uint64_t> &ptr,
                hipStream_t s) {
   const size_t W = 2 * static_cast<size_t>(k) + kSlotR;
-  // One launch per rebuilt-row count, the launches spread over the caller's
-  // stream and two fork streams so they run concurrently: no launch waits
-  // out another's tail, and a small group (the few chunks that lost many
-  // shares) overlaps the big ones.
+  // Items of up to kMixR rebuilt rows (a download's chunks: most lost 0-3
+  // data shares, each chunk a different set) go to ONE mixed-row launch; each
+  // row count above that gets a launch of its own. Everything on the
+  // caller's stream, in order: after the address-space fix the launches are
+  // HBM-bound, and sequential launches measured faster than the same ones
+  // fanned out over three streams (67.7 vs 62.0 % of peak, descbench).
   struct Group {
     uint32_t r = 0, rec_q = 0;
+    bool mix = false;
     std::vector<uint32_t> items;
     size_t tab_off = 0, rec_off = 0, ntab = 0;
     std::unordered_map<const Pattern *, size_t> tab_at;  // pattern -> its tables (PermTabs)
   };
   std::vector<Group> by_r(kSlotR + 1);
+  Group mixg;
+  mixg.mix = true;
+  mixg.r = kMixR;
   for (uint32_t i = 0; i < pats.size(); i++) {
     const uint32_t e = static_cast<uint32_t>(pats[i]->missing.size());
     if (e > static_cast<uint32_t>(kSlotR)) return fail(ctx, STORB_RS_EINVAL, "apply_desc: > 16 rows");
-    if (e || copy) by_r[e].items.push_back(i);
+    if (!e && !copy) continue;
+    (e <= kMixR ? mixg : by_r[e]).items.push_back(i);
   }
   std::vector<Group *> groups;
-  for (uint32_t e = 0; e <= static_cast<uint32_t>(kSlotR); e++)
+  if (!mixg.items.empty()) groups.push_back(&mixg);
+  for (uint32_t e = kMixR + 1; e <= static_cast<uint32_t>(kSlotR); e++)
     if (!by_r[e].items.empty()) {
       by_r[e].r = e;
       groups.push_back(&by_r[e]);
     }
   if (groups.empty()) return STORB_RS_OK;
-  std::stable_sort(groups.begin(), groups.end(), [](const Group *a, const Group *b) {
-    return a->items.size() > b->items.size();
-  });
   size_t total = 0;
   uint64_t tiles = 0;
   const uint64_t tps = (block / 16 + kThreadsTable - 1) / kThreadsTable;
@@ -147,25 +154,18 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
     uint64_t *rec = reinterpret_cast<uint64_t *>(h + g->rec_off);
     for (uint32_t i : g->items) {
       const uint64_t *src = &ptr[i * W];
-      rec[0] = static_cast<uint64_t>(g->tab_at[pats[i]]);
+      const uint64_t e = pats[i]->missing.size();
+      rec[0] = static_cast<uint64_t>(g->tab_at[pats[i]]) | (e << 32);
       std::memcpy(rec + 1, src, static_cast<size_t>(k) * 8);
-      std::memcpy(rec + 1 + k, src + k, static_cast<size_t>(g->r) * 8);
+      std::memset(rec + 1 + k, 0, static_cast<size_t>(g->r) * 8);
+      std::memcpy(rec + 1 + k, src + k, static_cast<size_t>(e) * 8);
       if (copy) std::memcpy(rec + 1 + k + g->r, src + k + kSlotR, static_cast<size_t>(k) * 8);
       rec += g->rec_q;
     }
   }
-  const int nfork = static_cast<int>(std::min<size_t>(groups.size() - 1, kDescForks));
-  for (int f = 0; f < nfork; f++)
-    if (!ctx->fork[f]) {
-      HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->fork[f], hipStreamNonBlocking));
-      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->fork_ev[f], hipEventDisableTiming));
-    }
-  if (!ctx->fork_start && nfork)
-    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->fork_start, hipEventDisableTiming));
-  uint8_t *dev = ctx->desc_dev[slot].p;
-  hipError_t e = hipMemcpyAsync(dev, h, total, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess && nfork) e = hipEventRecord(ctx->fork_start, s);
-  for (int f = 0; e == hipSuccess && f < nfork; f++) e = hipStreamWaitEvent(ctx->fork[f], ctx->fork_start, 0);
+  uint8_t *dev = ctx->desc_dev[slot].p, *hd = nullptr;
+  HIP_TRY(ctx, host_dev_ptr(h, &hd));
+  hipError_t e = launch_copy16(dev, hd, total, s);
   for (size_t gi = 0; e == hipSuccess && gi < groups.size(); gi++) {
     const Group &g = *groups[gi];
     DescArgs a{};
@@ -178,16 +178,10 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
     a.nitems = static_cast<uint32_t>(g.items.size());
     a.copy = copy ? 1u : 0u;
     a.rec_qwords = g.rec_q;
-    const int lane = static_cast<int>(gi % (nfork + 1));  // 0 = the caller's stream
-    e = launch_apply_desc(a, lane ? ctx->fork[lane - 1] : s);
+    a.mix = g.mix ? 1u : 0u;
+    e = launch_apply_desc(a, s);
   }
-  // join (also after a failed launch: earlier ones may be queued), then the
-  // slot's reuse event on the caller's stream
-  for (int f = 0; f < nfork; f++) {
-    const hipError_t r1 = hipEventRecord(ctx->fork_ev[f], ctx->fork[f]);
-    const hipError_t r2 = r1 == hipSuccess ? hipStreamWaitEvent(s, ctx->fork_ev[f], 0) : r1;
-    if (e == hipSuccess) e = r2;
-  }
+  // the slot's reuse event (also after a failed launch: earlier ones may be queued)
   const hipError_t er = hipEventRecord(ctx->desc_ev[slot], s);
   if (e != hipSuccess) return hip_fail(ctx, e, "apply_desc");
   if (er != hipSuccess) return hip_fail(ctx, er, "hipEventRecord(descriptors)");

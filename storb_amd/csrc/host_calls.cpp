@@ -7,6 +7,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -15,6 +16,37 @@
 
 using namespace storb_rs;
 using namespace storb_rs::detail;
+
+// Stage timestamps of the single calls, only in a build with
+// -DSTORB_RS_CALL_TRACE (tools/callprobe.cpp's tracing build); the product
+// build compiles the marks away.
+#ifdef STORB_RS_CALL_TRACE
+#include <chrono>
+namespace {
+struct Mark {
+  const char *what;
+  double us;
+};
+thread_local std::vector<Mark> g_marks;
+void tmark(const char *w) {
+  g_marks.push_back({w, std::chrono::duration<double, std::micro>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count()});
+}
+}  // namespace
+extern "C" int storb_rs_debug_marks(const char **what, double *us, int max) {
+  int n = 0;
+  for (const Mark &m : g_marks) {
+    if (n == max) break;
+    what[n] = m.what;
+    us[n++] = m.us;
+  }
+  g_marks.clear();
+  return n;
+}
+#define TMARK(w) tmark(w)
+#else
+#define TMARK(w) ((void)0)
+#endif
 
 namespace storb_rs {
 namespace detail {
@@ -25,6 +57,54 @@ namespace detail {
 // into pinned staging and unpacks slice t-1's outputs, so the staging copies
 // of pageable caller buffers overlap the kernel instead of adding to it.
 // q = 1 (small chunks) degenerates to pack -> launch -> sync -> unpack.
+// Completion of a slice's kernel. A blocking hipEventSynchronize returned
+// ~13 us after the kernel had ended (interrupt wake-up; stage marks of
+// tools/callprobe.cpp, profiles/r3k_calltrace.txt) -- a quarter of a 1 MiB
+// call -- and polling hipEventQuery slowed the calls down instead (runtime
+// lock contention: page-locked (4, 6) encode 43.5 -> 60 us). So the stream
+// itself writes a sequence number into page-locked memory once the slice's
+// kernel has completed (hipStreamWriteValue32, ordered after the kernel like
+// any stream operation), and the host spins on that word: no runtime call
+// while waiting. After 2 ms of spinning the wait falls back to a blocking
+// stream synchronisation (which also reports a device error).
+#ifndef STORB_RS_SLICE_EVENTS
+static int slice_signal(storb_rs_ctx *ctx, hipStream_t s, int t, uint32_t *seq) {
+  if (!ctx->flag_pin.p) {
+    HIP_TRY(ctx, ctx->flag_pin.ensure(kMaxSlices * 64));
+    std::memset(ctx->flag_pin.p, 0, kMaxSlices * 64);
+    HIP_TRY(ctx, host_dev_ptr(ctx->flag_pin.p, &ctx->flag_dev));
+  }
+  *seq = ++ctx->flag_seq;
+  HIP_TRY(ctx, hipStreamWriteValue32(s, ctx->flag_dev + t * 64, *seq, 0));
+  return STORB_RS_OK;
+}
+
+static int slice_wait(storb_rs_ctx *ctx, hipStream_t s, int t, uint32_t seq) {
+  const uint32_t *f = reinterpret_cast<const uint32_t *>(ctx->flag_pin.p + t * 64);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 1; __atomic_load_n(f, __ATOMIC_ACQUIRE) != seq; i++) {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+    if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      HIP_TRY(ctx, hipStreamSynchronize(s));
+      break;
+    }
+  }
+  return STORB_RS_OK;
+}
+#else  // the A/B baseline: one event per slice, blocking waits
+static int slice_signal(storb_rs_ctx *ctx, hipStream_t s, int t, uint32_t *) {
+  if (!ctx->slice_ev[t]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->slice_ev[t], hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventRecord(ctx->slice_ev[t], s));
+  return STORB_RS_OK;
+}
+static int slice_wait(storb_rs_ctx *ctx, hipStream_t, int t, uint32_t) {
+  HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[t]));
+  return STORB_RS_OK;
+}
+#endif
+
 int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)> &pack,
            const std::function<int(size_t, size_t)> &launch,
            const std::function<void(size_t, size_t)> &unpack) {
@@ -32,30 +112,35 @@ int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)
   if (q < 2) q = 1;
   const size_t slice = round_up((S + q - 1) / q, kAlign);
   q = static_cast<int>((S + slice - 1) / slice);
-  for (int t = 0; t < q; t++)
-    if (!ctx->slice_ev[t])
-      HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->slice_ev[t], hipEventDisableTiming));
   auto range = [&](int t, size_t &off, size_t &cnt) {
     off = static_cast<size_t>(t) * slice;
     cnt = std::min(slice, S - off);
   };
+  uint32_t seq[kMaxSlices] = {};
+  int rc;
   for (int t = 0; t < q; t++) {
     size_t off, cnt;
     range(t, off, cnt);
+    TMARK("pack");
     pack(off, cnt);
-    const int rc = launch(off, cnt);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipEventRecord(ctx->slice_ev[t], ctx->stream));
+    TMARK("launch");
+    if ((rc = launch(off, cnt))) return rc;
+    if ((rc = slice_signal(ctx, ctx->stream, t, &seq[t]))) return rc;
     if (t > 0) {
-      HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[t - 1]));
+      TMARK("wait");
+      if ((rc = slice_wait(ctx, ctx->stream, t - 1, seq[t - 1]))) return rc;
       range(t - 1, off, cnt);
+      TMARK("unpack");
       unpack(off, cnt);
     }
   }
   size_t off, cnt;
   range(q - 1, off, cnt);
-  HIP_TRY(ctx, hipEventSynchronize(ctx->slice_ev[q - 1]));
+  TMARK("wait");
+  if ((rc = slice_wait(ctx, ctx->stream, q - 1, seq[q - 1]))) return rc;
+  TMARK("unpack");
   unpack(off, cnt);
+  TMARK("end");
   return STORB_RS_OK;
 }
 

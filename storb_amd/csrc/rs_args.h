@@ -76,12 +76,23 @@ struct DescArgs {
   const PermTab *ptab;
   uint64_t block;  // bytes per share
   uint32_t k;
-  uint32_t r;
+  uint32_t r;      // output slots per record (mix: the most rows an item has)
   uint32_t tpw;    // tiles per workgroup
   uint32_t nitems;
   uint32_t copy;
   uint32_t rec_qwords;  // 1 + k + r (+ k with copy)
+  // mix = 1: items of different row counts (1..kMixR, 0 with copy) in one
+  // launch; item i's count is its record's rec[0] >> 32 and a workgroup runs
+  // the tile of that count. cap: resident workgroups per CU (0: the tuned
+  // value of the launch's row bucket).
+  uint32_t mix;
+  uint32_t cap;
 };
+
+// Rows per item a mixed-row descriptor launch takes: a download's chunks
+// mostly lost 0-3 data shares (tools/descbench.cpp, bench --erase-pattern
+// download); items with more rows get launches of their own.
+constexpr uint32_t kMixR = 4;
 
 // Launch shape of the bit-sliced kernels (rs_bitslice_core.h), shared by
 // the host launchers and the kernels. Grid: nstripes x tiles; a tile = T

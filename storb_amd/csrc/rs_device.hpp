@@ -107,10 +107,13 @@ __device__ __forceinline__ uint32_t gf_madd_perm(uint32_t acc, const PermTab &t,
 // vs 5.38 for the bit-sliced RS(16,8) encoder. (A single-launch timing
 // favours default stores, tools/hbm_probe.hip, because dirty lines left in
 // L2/MALL at kernel end are written back after the end event.)
-__device__ __forceinline__ u32x4 ld_stream(const u32x4 *p) {
+// (P: a generic or a global-address-space pointer to u32x4.)
+template <class P>
+__device__ __forceinline__ u32x4 ld_stream(P p) {
   return __builtin_nontemporal_load(p);
 }
-__device__ __forceinline__ void st_stream(u32x4 *p, u32x4 v) {
+template <class P>
+__device__ __forceinline__ void st_stream(P p, u32x4 v) {
 #if STORB_RS_NT_STORES
   __builtin_nontemporal_store(v, p);
 #else
@@ -126,34 +129,61 @@ __device__ __forceinline__ void st_stream(u32x4 *p, u32x4 v) {
 struct ArgsView {
   const ApplyArgs &a;
   uint32_t stripe;
-  __device__ __forceinline__ const uint8_t *in(int j) const {
-    return a.in[j] + static_cast<uint64_t>(stripe) * a.in_stride[j];
+  // (Pointers read from the kernel arguments: the compiler already knows
+  // they are global, and emits global_load / global_store.)
+  __device__ __forceinline__ const u32x4 *in(int j) const {
+    return reinterpret_cast<const u32x4 *>(a.in[j] + static_cast<uint64_t>(stripe) * a.in_stride[j]);
   }
-  __device__ __forceinline__ uint8_t *out(int i) const {
-    return a.out[i] + static_cast<uint64_t>(stripe) * a.out_stride[i];
+  __device__ __forceinline__ u32x4 *out(int i) const {
+    return reinterpret_cast<u32x4 *>(a.out[i] + static_cast<uint64_t>(stripe) * a.out_stride[i]);
   }
   __device__ __forceinline__ bool has_copy(int j) const { return a.copy[j] != nullptr; }
-  __device__ __forceinline__ uint8_t *copy(int j) const {
-    return a.copy[j] + static_cast<uint64_t>(stripe) * a.copy_stride[j];
+  __device__ __forceinline__ u32x4 *copy(int j) const {
+    return reinterpret_cast<u32x4 *>(a.copy[j] + static_cast<uint64_t>(stripe) * a.copy_stride[j]);
   }
   __device__ __forceinline__ bool accumulate() const { return a.accumulate != 0; }
 };
 
+// Global (address space 1) and constant (address space 4) pointers. The
+// descriptor kernel reads its shares' addresses from memory, where the
+// compiler cannot tell they are global: as generic pointers every share load
+// and store became flat_load / flat_store, which count against lgkmcnt too,
+// so each LDS table read waited for the in-flight share loads (no double
+// buffering: 41 % of HBM peak against 77 % for the same tile on kernel
+// arguments, tools/descbench.cpp). And the record, read through a generic
+// pointer, came in as per-lane global_load_dwordx2 instead of s_load.
+typedef u32x4 __attribute__((address_space(1))) gu32x4;
+typedef const uint64_t __attribute__((address_space(4))) cu64;
+
 struct DescView {
-  const uint64_t *rec;  // this item's record (wave-uniform: scalar loads)
-  uint32_t k, ro;       // ro = output slots per record
-  __device__ __forceinline__ const uint8_t *in(int j) const {
-    return reinterpret_cast<const uint8_t *>(rec[1 + j]);
+  cu64 *rec;        // this item's record (wave-uniform: scalar loads)
+  uint32_t k, ro;   // ro = output slots per record
+  __device__ __forceinline__ const gu32x4 *in(int j) const {
+    return (const gu32x4 *)(rec[1 + j]);
   }
-  __device__ __forceinline__ uint8_t *out(int i) const {
-    return reinterpret_cast<uint8_t *>(rec[1 + k + i]);
+  __device__ __forceinline__ gu32x4 *out(int i) const {
+    return (gu32x4 *)(rec[1 + k + i]);
   }
   __device__ __forceinline__ bool has_copy(int j) const { return rec[1 + k + ro + j] != 0; }
-  __device__ __forceinline__ uint8_t *copy(int j) const {
-    return reinterpret_cast<uint8_t *>(rec[1 + k + ro + j]);
+  __device__ __forceinline__ gu32x4 *copy(int j) const {
+    return (gu32x4 *)(rec[1 + k + ro + j]);
   }
   __device__ __forceinline__ bool accumulate() const { return false; }
 };
+
+// A coefficient's table from LDS / a generic pointer, or field by field
+// from a constant-address-space one (wave-uniform: s_load).
+__device__ __forceinline__ PermTab get_tab(const PermTab *p) { return *p; }
+template <class P>
+__device__ __forceinline__ PermTab get_tab(P p) {
+  PermTab t{};
+  t.t0lo = p->t0lo;
+  t.t0hi = p->t0hi;
+  t.t1lo = p->t1lo;
+  t.t1hi = p->t1hi;
+  t.t2 = p->t2;
+  return t;
+}
 
 // Inputs are consumed in groups of up to 8 shares; the next group's
 // dwordx4 loads are issued before the current group is multiplied (double
@@ -166,7 +196,7 @@ __device__ __forceinline__ void load_group(const V &v, uint32_t k, uint32_t cols
   for (int jj = 0; jj < G; jj++) {
     const int j = g * G + jj;
     if (j >= static_cast<int>(k)) continue;
-    const u32x4 *p = reinterpret_cast<const u32x4 *>(v.in(j));
+    const auto p = v.in(j);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t c = c0 + u * T;
@@ -194,7 +224,7 @@ __device__ __forceinline__ void copy_group(const V &v, uint32_t k, uint32_t cols
   for (int jj = 0; jj < G; jj++) {
     const int j = g * G + jj;
     if (j >= static_cast<int>(k) || !v.has_copy(j)) continue;
-    u32x4 *q = reinterpret_cast<u32x4 *>(v.copy(j));
+    const auto q = v.copy(j);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t c = c0 + u * T;
@@ -204,8 +234,8 @@ __device__ __forceinline__ void copy_group(const V &v, uint32_t k, uint32_t cols
 }
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD,
-          bool COPY = false, class V>
-__device__ __forceinline__ void perm_tile(const V &v, const PermTab *tabs, uint32_t k,
+          bool COPY = false, class V, class TP>
+__device__ __forceinline__ void perm_tile(const V &v, TP tabs, uint32_t k,
                                           uint32_t r, uint32_t cols, uint32_t c0) {
   constexpr int NG = KM / G;
   u32x4 buf[2][G][U];
@@ -248,8 +278,8 @@ __device__ __forceinline__ void perm_tile(const V &v, const PermTab *tabs, uint3
             }
 #pragma unroll
         for (int i = 0; i < RM; i++) {
-          const PermTab ta = tabs[j * RM + i];
-          const PermTab tb = two ? tabs[(j + 1) * RM + i] : PermTab{};
+          const PermTab ta = get_tab(tabs + (j * RM + i));
+          const PermTab tb = two ? get_tab(tabs + ((j + 1) * RM + i)) : PermTab{};
 #pragma unroll
           for (int u = 0; u < U; u++)
 #pragma unroll
@@ -287,7 +317,7 @@ __device__ __forceinline__ void perm_tile(const V &v, const PermTab *tabs, uint3
         // guards made every coefficient wait out a full load latency).
         PermTab t[RM];
 #pragma unroll
-        for (int i = 0; i < RM; i++) t[i] = tabs[j * RM + i];
+        for (int i = 0; i < RM; i++) t[i] = get_tab(tabs + (j * RM + i));
 #pragma unroll
         for (int i = 0; i < RM; i++)
 #pragma unroll
@@ -303,7 +333,7 @@ __device__ __forceinline__ void perm_tile(const V &v, const PermTab *tabs, uint3
 #pragma unroll
   for (int i = 0; i < RM; i++) {
     if (i >= static_cast<int>(r)) continue;
-    u32x4 *q = reinterpret_cast<u32x4 *>(v.out(i));
+    const auto q = v.out(i);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t c = c0 + u * T;
@@ -353,9 +383,10 @@ __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
 // rs_apply_perm does over `tpw` consecutive tiles of the stripe: the record
 // -> tables -> first loads chain (~1-2 us of dependent latency a workgroup
 // of one tile pays before its first byte streams) is paid once per tpw tiles.
-template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false,
-          bool COPY = false>
-__global__ __launch_bounds__(T) void rs_apply_desc(const DescArgs a) {
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR, bool COPY,
+          int RL = RM>
+__device__ __forceinline__ void desc_body(const DescArgs &a, cu64 *rec, uint32_t r,
+                                          PermTab *lds_ptab) {
   constexpr uint32_t TILE = T * U;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + TILE - 1) / TILE;
@@ -363,26 +394,73 @@ __global__ __launch_bounds__(T) void rs_apply_desc(const DescArgs a) {
   const uint32_t item = blockIdx.x / wps;
   const uint32_t t0 = (blockIdx.x - item * wps) * a.tpw;
   const uint32_t t1 = t0 + a.tpw < tps ? t0 + a.tpw : tps;
-  const uint64_t *rec = a.desc + static_cast<uint64_t>(item) * a.rec_qwords;
-  const PermTab *tabs = a.ptab + (rec[0] & 0xFFFFFFFFu);
-  if constexpr (TL) {
-    __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * RM];
-    const uint32_t n16 = (COPY && a.r == 0) ? 0u : a.k * RM * (sizeof(PermTab) / 16);
-    for (uint32_t t = threadIdx.x; t < n16; t += T)
-      reinterpret_cast<u32x4 *>(lds_ptab)[t] = reinterpret_cast<const u32x4 *>(tabs)[t];
-    __syncthreads();
-    tabs = lds_ptab;
-  }
+  typedef const PermTab __attribute__((address_space(4))) cPermTab;
+  cPermTab *gtabs = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
   const DescView v{rec, a.k, a.r};
-  for (uint32_t t = t0; t < t1; t++) {
-    const uint32_t base = t * TILE;
-    if (base + TILE <= cols)
-      perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, a.r, cols,
-                                                        base + threadIdx.x);
-    else
-      perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, a.r, cols,
-                                                       base + threadIdx.x);
+  auto run = [&](auto tabs0) {
+    for (uint32_t t = t0; t < t1; t++) {
+      // The tables are the same for every tile: without this opaque zero,
+      // loop-invariant code motion hoists all k x RM of them out of the tile
+      // loop into VGPRs (256 VGPRs and scratch from 3 rows at k = 16).
+      uint32_t zero = 0;
+      asm volatile("" : "+s"(zero));
+      const auto tabs = tabs0 + zero;
+      const uint32_t base = t * TILE;
+      if (base + TILE <= cols)
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, r, cols,
+                                                          base + threadIdx.x);
+      else
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, r, cols,
+                                                         base + threadIdx.x);
+    }
+  };
+  if constexpr (TL) {
+    const uint32_t n16 = (COPY && r == 0) ? 0u : a.k * RM * (sizeof(PermTab) / 16);
+    typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
+    for (uint32_t t = threadIdx.x; t < n16; t += T)
+      reinterpret_cast<u32x4 *>(lds_ptab)[t] = ((gcu32x4 *)(gtabs))[t];
+    __syncthreads();
+    run(static_cast<const PermTab *>(lds_ptab));
+  } else {
+    run(gtabs);  // wave-uniform table reads: s_load
   }
+}
+
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false,
+          bool COPY = false>
+__global__ __launch_bounds__(T) void rs_apply_desc(const DescArgs a) {
+  __shared__ __attribute__((aligned(16))) PermTab lds_ptab[TL ? KM * RM : 1];
+  const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + T * U - 1) / (T * U);
+  const uint32_t item = blockIdx.x / ((tps + a.tpw - 1) / a.tpw);
+  cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
+  desc_body<KM, RM, T, U, BAR, G, TL, PAIR, COPY>(a, rec, a.r, lds_ptab);
+}
+
+// Mixed row counts in one launch (DescArgs::mix): each workgroup reads its
+// item's count and runs that count's tile (the Tune of that bucket), so a
+// download's chunks -- most lost 1-3 data shares, each a different set --
+// are one launch: no per-count launch gaps and tails, and no 3-row VALU
+// spent on a 1-row item. Registers: the largest branch's.
+template <int KM, bool COPY>
+__global__ __launch_bounds__(kThreads) void rs_apply_desc_mix(const DescArgs a) {
+  using T1 = Tune<KM, 1>;
+  __shared__ __attribute__((aligned(16))) PermTab lds_ptab[T1::TL ? KM * kMixR : 1];
+  const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + kThreads - 1) / kThreads;
+  const uint32_t item = blockIdx.x / ((tps + a.tpw - 1) / a.tpw);
+  cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
+  const uint32_t r = static_cast<uint32_t>(rec[0] >> 32);
+#define STORB_MIX_CASE(R)                                                                   \
+  {                                                                                         \
+    using C = Tune<KM, R>;                                                                  \
+    static_assert(C::T == kThreads && C::U == 1, "mixed launch: one tile shape");           \
+    desc_body<KM, R, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR, COPY>(a, rec, r, lds_ptab);  \
+    return;                                                                                 \
+  }
+  if (r <= 1) STORB_MIX_CASE(1)
+  if (r == 2) STORB_MIX_CASE(2)
+  if (r == 3) STORB_MIX_CASE(3)
+  STORB_MIX_CASE(4)
+#undef STORB_MIX_CASE
 }
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
@@ -411,7 +489,7 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
   const uint64_t blocks = ((tps + a.tpw - 1) / a.tpw) * a.nitems;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
-  const size_t dyn = cap_lds(wg_cap(a.copy ? occ_copy : occ),
+  const size_t dyn = cap_lds(a.cap ? static_cast<int>(a.cap) : wg_cap(a.copy ? occ_copy : occ),
                              TL ? sizeof(PermTab) * KM * RM : 0);
   if (a.copy) {
     if constexpr (KM <= static_cast<int>(kCopyMaxK))
@@ -423,8 +501,34 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
   return launch_lds<rs_apply_desc<KM, RM, T, U, BAR, G, TL, PAIR>>(blocks, T, dyn, s, a);
 }
 
+// Default resident-workgroup cap of a mixed-row launch (DescArgs::cap = 0).
+// k = 16 download mix (tools/descbench.cpp, profiles/r3j_descbench.txt):
+// capped at 2 or 3 per CU 61.5 %, at 4 72.1 %, uncapped 72.4 % of 8 TB/s.
+// k <= 4 keeps the RS(4,2) table kernel's measured cap of 4.
+constexpr int mix_occ(int KM) { return KM <= 4 ? Tune<4, 2>::OCC : 0; }
+
+template <int KM>
+hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
+  constexpr uint64_t TILE = kThreads;
+  const uint64_t tps = ((a.block >> 4) + TILE - 1) / TILE;
+  if (a.tpw == 0) return hipErrorInvalidValue;
+  const uint64_t blocks = ((tps + a.tpw - 1) / a.tpw) * a.nitems;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+  const size_t dyn = cap_lds(a.cap ? static_cast<int>(a.cap) : mix_occ(KM),
+                             Tune<KM, 1>::TL ? sizeof(PermTab) * KM * kMixR : 0);
+  if (a.copy) {
+    if constexpr (KM <= static_cast<int>(kCopyMaxK))
+      return launch_lds<rs_apply_desc_mix<KM, true>>(blocks, kThreads, dyn, s, a);
+    else
+      return hipErrorInvalidValue;
+  }
+  return launch_lds<rs_apply_desc_mix<KM, false>>(blocks, kThreads, dyn, s, a);
+}
+
 template <int KM>
 hipError_t go_desc_r(const DescArgs &a, hipStream_t s) {
+  if (a.mix) return launch_desc_mix<KM>(a, s);
   switch (rows_bucket(a.r)) {
 #define STORB_DESC_CASE(R)                                                                 \
   case R: {                                                                                \

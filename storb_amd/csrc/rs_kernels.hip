@@ -3,6 +3,8 @@
 // are in rs_device.hpp; their instantiations in rs_perm_k*.hip / rs_lds.hip.
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "rs_device.hpp"
 
 namespace storb_rs {
@@ -115,7 +117,7 @@ hipError_t launch_apply(const ApplyArgs &a, Variant v, hipStream_t s) {
 
 hipError_t launch_apply_desc(const DescArgs &a, hipStream_t s) {
   if (a.k == 0 || a.k > kSlotK || a.r > kSlotR || (a.copy && a.k > kCopyMaxK) ||
-      (a.r == 0 && !a.copy) || a.block % 16 || a.tpw == 0 ||
+      (a.r == 0 && !a.copy) || a.block % 16 || a.tpw == 0 || (a.mix && a.r != kMixR) ||
       a.rec_qwords != 1 + a.k + a.r + (a.copy ? a.k : 0))
     return hipErrorInvalidValue;
   if (a.block == 0 || a.nitems == 0) return hipSuccess;
@@ -127,6 +129,28 @@ hipError_t launch_apply_desc(const DescArgs &a, hipStream_t s) {
     case 16: return dispatch_desc_k16(a, s);
     default: return dispatch_desc_k32(a, s);
   }
+}
+
+// Descriptor upload (decode_stripes.cpp apply_desc): page-locked host
+// memory -> device, read over PCIe by a kernel on the launch stream. An SDMA
+// copy (hipMemcpyAsync) in front of the decode kernels kept them waiting on
+// the copy engine's start-up and completion signalling.
+__global__ __launch_bounds__(kThreads) void copy_u32x4_kernel(u32x4 *dst, const u32x4 *src,
+                                                              uint64_t n) {
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(kThreads) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * kThreads)
+    dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+hipError_t launch_copy16(void *dst, const void *src, uint64_t bytes, hipStream_t s) {
+  if (bytes % 16 || (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 16)
+    return hipErrorInvalidValue;
+  const uint64_t n = bytes / 16;
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>(256, (n + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(copy_u32x4_kernel, dim3(blocks), dim3(kThreads), 0, s,
+                     static_cast<u32x4 *>(dst), static_cast<const u32x4 *>(src), n);
+  return hipGetLastError();
 }
 
 hipError_t launch_fill_splitmix(uint8_t *d, uint64_t obj_len, uint32_t nobj,

@@ -94,6 +94,9 @@ hipError_t launch_encode_bitslice(const ApplyArgs &a, uint32_t n, hipStream_t s)
 hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
                                uint64_t stride, uint8_t *out, hipStream_t s);
 
+// dst (device) <- src (device-accessible, e.g. page-locked host), 16-B
+// aligned, bytes % 16 == 0, by a kernel on stream s.
+hipError_t launch_copy16(void *dst, const void *src, uint64_t bytes, hipStream_t s);
 hipError_t launch_fill_splitmix(uint8_t *d, uint64_t obj_len, uint32_t nobj,
                                 uint64_t obj_stride, uint64_t seed_base,
                                 hipStream_t s);

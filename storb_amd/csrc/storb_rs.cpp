@@ -12,6 +12,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -529,14 +530,6 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
-  for (int f = 0; f < kDescForks; f++) {
-    if (ctx->fork[f]) {
-      (void)hipStreamSynchronize(ctx->fork[f]);
-      (void)hipStreamDestroy(ctx->fork[f]);
-    }
-    if (ctx->fork_ev[f]) (void)hipEventDestroy(ctx->fork_ev[f]);
-  }
-  if (ctx->fork_start) (void)hipEventDestroy(ctx->fork_start);
   for (auto &e : ctx->desc_ev)  // descriptor launches may run on callers' streams
     if (e) {
       (void)hipEventSynchronize(e);

@@ -27,3 +27,16 @@ def ctx():
     c.default_stream = torch.cuda.current_stream(0).cuda_stream
     yield c
     c.close()
+
+
+@pytest.fixture(autouse=True)
+def _device_clean_after_gpu_test(request):
+    """After every GPU test, wait for the device: a fault left by that test's
+    asynchronous work (queued kernels, async ops, host functions) is then
+    reported against it, not against whichever test next touches the GPU."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()

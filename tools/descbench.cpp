@@ -9,6 +9,8 @@
 //   * the same fanned out over 3 streams;
 //   * uniform reference: every stripe with 2 lost, one table-kernel launch
 //     (storb_rs_decode_batch_dev with the PERM variant).
+//   * one mixed-row launch (DescArgs::mix) over the resident-workgroup cap;
+//   * the product call's host time;
 // Bytes = sum over stripes with e > 0 of (k + e) * B. Performance only (the
 // coefficients are random); bit-exactness is tests/test_gpu_patterns.py's.
 // build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/descbench.cpp -Iinclude \
@@ -17,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -163,6 +166,63 @@ int main(int argc, char **argv) {
           }
         }, bytes))
       return 1;
+  }
+  // one mixed-row launch (DescArgs::mix): records with kMixR output slots,
+  // rec[0] = table offset | rows << 32; resident-workgroup cap swept
+  std::vector<uint64_t> mrec;
+  std::vector<PermTab> mtab;
+  for (uint32_t s = 0; s < N; s++) {
+    const uint32_t e = es[s];
+    if (!e) continue;
+    const uint64_t off = mtab.size();
+    for (uint32_t j = 0; j < k * e; j++) mtab.push_back(perm_tab(uint8_t(rng() | 1)));
+    mrec.push_back(off | (uint64_t(e) << 32));
+    for (uint32_t c = 0; c < k; c++) {
+      const uint32_t id = surv[s][c];
+      mrec.push_back(reinterpret_cast<uint64_t>(
+          id < k ? d + s * k * B + id * B : p + s * (n - k) * B + (id - k) * B));
+    }
+    for (uint32_t r = 0; r < kMixR; r++)
+      mrec.push_back(r < e ? reinterpret_cast<uint64_t>(d + s * k * B + lost[s][r] * B) : 0);
+  }
+  uint64_t *dmrec = nullptr;
+  PermTab *dmtab = nullptr;
+  CK(hipMalloc(&dmrec, mrec.size() * 8));
+  CK(hipMalloc(&dmtab, mtab.size() * sizeof(PermTab)));
+  CK(hipMemcpy(dmrec, mrec.data(), mrec.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dmtab, mtab.data(), mtab.size() * sizeof(PermTab), hipMemcpyHostToDevice));
+  for (uint32_t cap : {0u, 2u, 3u, 4u, 8u}) {
+    for (uint32_t tpw : {1u, 2u}) {
+      DescArgs a{};
+      a.desc = dmrec;
+      a.ptab = dmtab;
+      a.block = B;
+      a.k = k;
+      a.r = kMixR;
+      a.tpw = tpw;
+      a.nitems = N - 13;
+      a.rec_qwords = 1 + k + kMixR;
+      a.mix = 1;
+      a.cap = cap;
+      char name[96];
+      std::snprintf(name, sizeof(name), "one mixed-row launch, cap %u%s, tpw %u", cap,
+                    cap ? "" : " (default)", tpw);
+      if (timeit(name, [&] { (void)launch_apply_desc(a, st[0]); }, bytes)) return 1;
+    }
+  }
+  // host time of the product call (patterns, records, upload, launches)
+  {
+    std::vector<double> hus;
+    for (int r = 0; r < reps; r++) {
+      CK(hipStreamSynchronize(st[0]));
+      const auto t0 = std::chrono::steady_clock::now();
+      storb_rs_decode_stripes_dev(ctx, k, n, B, N, flat.data(), cnt.data(), d, 0, p, 0, d, 0, st[0]);
+      hus.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    CK(hipStreamSynchronize(st[0]));
+    std::sort(hus.begin(), hus.end());
+    std::printf("product call host time (returns before the kernels end): median %.1f us\n",
+                hus[hus.size() / 2]);
   }
   // uniform reference: 2 lost everywhere, table kernel
   storb_rs_set_kernel(ctx, STORB_RS_KERNEL_PERM);
