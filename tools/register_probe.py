@@ -48,6 +48,7 @@ def main():
         attr = (C.c_ubyte * 128)()
         e2 = hip.hipPointerGetAttributes(attr, C.c_void_p(addr))
         mtype = int.from_bytes(bytes(attr[:4]), "little")
+        hip.hipGetLastError()  # the failed queries set HIP's last error; torch checks it
         return {"hipHostGetDevicePointer": e1, "dev": d.value, "hipPointerGetAttributes": e2,
                 "memoryType": mtype}
 
