@@ -94,9 +94,13 @@ struct Tables {
   std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // last use per stream
   uint64_t tick = 0;              // LRU clock
   ~Tables() {
-    // Context teardown only (its streams are drained first); eviction frees
-    // asynchronously instead (storb_rs.cpp evict_tables).
-    if (dev) (void)hipFree(dev);
+    // dev is pool memory (hipMallocAsync): eviction and context teardown
+    // return it with hipFreeAsync (storb_rs.cpp release_table); only a table
+    // whose release failed gets here with it, freed the same way.
+    if (dev) {
+      (void)hipFreeAsync(dev, nullptr);
+      (void)hipStreamSynchronize(nullptr);
+    }
     if (uploaded) (void)hipEventDestroy(uploaded);
     for (auto &u : uses) (void)hipEventDestroy(u.second);
   }
@@ -171,6 +175,13 @@ struct storb_rs_ctx {
   storb_rs::detail::PinBuf flag_pin;
   uint8_t *flag_dev = nullptr;
   uint32_t flag_seq = 0;
+  // Streamed single calls (host_calls.cpp streamed): ready / done words
+  // (page-locked, 64 B apart), per-slice device counters and their expected
+  // base values (the counters only ever count up).
+  storb_rs::detail::PinBuf sword_pin;
+  uint8_t *sword_dev = nullptr;
+  storb_rs::detail::DevBuf scnt;
+  uint32_t sbase[storb_rs::kMaxStreamSlices] = {};
   // Decode patterns by (k, n, slot share indices) and the ring the
   // per-stripe descriptors go through: page-locked source, device copy;
   // desc_ev[i]: the launches of that slot's last use have completed.

@@ -125,6 +125,7 @@ int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)
     pack(off, cnt);
     TMARK("launch");
     if ((rc = launch(off, cnt))) return rc;
+    TMARK("signal");
     if ((rc = slice_signal(ctx, ctx->stream, t, &seq[t]))) return rc;
     if (t > 0) {
       TMARK("wait");
@@ -141,6 +142,127 @@ int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)
   TMARK("unpack");
   unpack(off, cnt);
   TMARK("end");
+  return STORB_RS_OK;
+}
+
+// The streamed single call (StreamArgs, rs_args.h; rs_apply_stream): one
+// launch, issued BEFORE the host packs anything, whose workgroups wait for
+// their slice's ready word; the host packs slice after slice and publishes
+// each, then unpacks each slice as its done word turns. Per call: one
+// launch, no stream synchronisation, the launch latency hidden behind the
+// packing of slice 0. For k <= 8 and 1..8 rows on the table kernel (Storb's
+// chunks up to 4 MiB, (2,3) (4,6) (8,12)); kNotStreamed = not applicable or
+// not completed -- the caller then runs the sliced path, which recomputes
+// everything (the caller's buffers are not touched by a failed attempt
+// except staging and, for direct outputs, rows the classic path rewrites).
+constexpr int kNotStreamed = -1;
+
+int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
+             const uint8_t *const *in, uint8_t *const *out, size_t S,
+             const std::function<void(size_t, size_t)> &pack,
+             const std::function<void(size_t, size_t)> &unpack) {
+  if (ctx->variant != STORB_RS_KERNEL_AUTO || k == 0 || k > 8 || rows == 0 || rows > 8 ||
+      S % kAlign)
+    return kNotStreamed;
+  const uint32_t cols = static_cast<uint32_t>(S / 16);
+  // 64 KiB of every share per slice, at most kMaxStreamSlices slices
+  uint32_t slice_cols = 4096;
+  if ((cols + slice_cols - 1) / slice_cols > static_cast<uint32_t>(kMaxStreamSlices))
+    slice_cols = static_cast<uint32_t>(
+        round_up((cols + kMaxStreamSlices - 1) / kMaxStreamSlices, kThreadsTable));
+  const uint32_t nsl = (cols + slice_cols - 1) / slice_cols;
+  hipStream_t s = ctx->stream;
+  if (!ctx->sword_pin.p) {
+    HIP_TRY(ctx, ctx->sword_pin.ensure(2 * kMaxStreamSlices * 64));
+    std::memset(ctx->sword_pin.p, 0, 2 * kMaxStreamSlices * 64);
+    HIP_TRY(ctx, host_dev_ptr(ctx->sword_pin.p, &ctx->sword_dev));
+    HIP_TRY(ctx, ctx->scnt.ensure(kMaxStreamSlices * sizeof(uint32_t)));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->scnt.p, 0, kMaxStreamSlices * sizeof(uint32_t), s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    std::memset(ctx->sbase, 0, sizeof(ctx->sbase));
+  }
+  Tables *t = nullptr;
+  int rc = get_tables(ctx, k, rows, coef, s, &t);
+  if (rc) return rc;
+  ApplyArgs a{};
+  a.k = k;
+  a.r = rows;
+  for (uint32_t j = 0; j < k; j++) {
+    a.in[j] = in[j];
+    a.in_stride[j] = S;
+  }
+  for (uint32_t i = 0; i < rows; i++) {
+    a.out[i] = out[i];
+    a.out_stride[i] = S;
+  }
+  a.ptab = reinterpret_cast<const PermTab *>(t->dev);
+  a.tab_rows = static_cast<uint32_t>(rows_bucket(rows));
+  a.block = S;
+  a.nstripes = 1;
+  StreamArgs st{};
+  uint32_t *words = reinterpret_cast<uint32_t *>(ctx->sword_dev);
+  st.ready = words;
+  st.done = words + kMaxStreamSlices * 16;
+  st.cnt = reinterpret_cast<uint32_t *>(ctx->scnt.p);
+  st.seq = ++ctx->flag_seq;
+  st.slice_cols = slice_cols;
+  st.nslices = nsl;
+  st.timeout_ticks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
+  uint32_t tiles[kMaxStreamSlices] = {};
+  for (uint32_t i = 0; i < nsl; i++) {
+    const uint32_t len = std::min(slice_cols, cols - i * slice_cols);
+    tiles[i] = (len + static_cast<uint32_t>(kThreadsTable) - 1) / static_cast<uint32_t>(kThreadsTable);
+    st.target[i] = ctx->sbase[i] + tiles[i];
+  }
+  const hipError_t le = launch_apply_stream(a, st, s);
+  if (le == hipErrorInvalidValue) return kNotStreamed;  // nothing was queued
+  HIP_TRY(ctx, le);
+  rc = tables_used(ctx, t, s);
+  if (rc) return rc;
+  uint32_t *ready_h = reinterpret_cast<uint32_t *>(ctx->sword_pin.p);
+  const uint32_t *done_h = ready_h + kMaxStreamSlices * 16;
+  auto range = [&](uint32_t i, size_t &off, size_t &cnt) {
+    off = static_cast<size_t>(i) * slice_cols * 16;
+    cnt = std::min(static_cast<size_t>(slice_cols) * 16, S - off);
+  };
+  for (uint32_t i = 0; i < nsl; i++) {
+    size_t off, cnt;
+    range(i, off, cnt);
+    TMARK("pack");
+    pack(off, cnt);
+    __atomic_store_n(ready_h + 16 * i, st.seq, __ATOMIC_RELEASE);
+  }
+  bool ok = true;
+  for (uint32_t i = 0; i < nsl && ok; i++) {
+    TMARK("wait");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1; __atomic_load_n(done_h + 16 * i, __ATOMIC_ACQUIRE) != st.seq; it++) {
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+      if ((it & 1023) == 0 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
+        // the GPU may just be busy with other streams' work: drain, look again
+        HIP_TRY(ctx, hipStreamSynchronize(s));
+        ok = __atomic_load_n(done_h + 16 * i, __ATOMIC_ACQUIRE) == st.seq;
+        break;
+      }
+    }
+    if (!ok) break;
+    size_t off, cnt;
+    range(i, off, cnt);
+    TMARK("unpack");
+    unpack(off, cnt);
+  }
+  TMARK("end");
+  if (!ok) {  // a workgroup gave up waiting: counters unknown -- reset, redo classically
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->scnt.p, 0, kMaxStreamSlices * sizeof(uint32_t), s));
+    HIP_TRY(ctx, hipStreamSynchronize(s));
+    std::memset(ctx->sbase, 0, sizeof(ctx->sbase));
+    return kNotStreamed;
+  }
+  for (uint32_t i = 0; i < nsl; i++) ctx->sbase[i] += tiles[i];
   return STORB_RS_OK;
 }
 
@@ -233,9 +355,21 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       HIP_TRY(ctx, hipStreamSynchronize(s));
       return STORB_RS_OK;
     }
-    return sliced(
-        ctx, S, [&](size_t off, size_t cnt) { if (!in_direct) pack(off, cnt); }, launch,
-        [&](size_t off, size_t cnt) { if (!out_direct) unpack(off, cnt); });
+    const std::function<void(size_t, size_t)> pk = [&](size_t off, size_t cnt) {
+      if (!in_direct) pack(off, cnt);
+    };
+    const std::function<void(size_t, size_t)> up = [&](size_t off, size_t cnt) {
+      if (!out_direct) unpack(off, cnt);
+    };
+    {
+      const std::vector<uint8_t> &enc = cached_enc(k, n);
+      std::vector<const uint8_t *> sin(k);
+      for (uint32_t j = 0; j < k; j++) sin[j] = dd + static_cast<size_t>(j) * S;
+      const int rs = streamed(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, sin.data(),
+                              pd.data(), S, pk, up);
+      if (rs != kNotStreamed) return rs;
+    }
+    return sliced(ctx, S, pk, launch, up);
   }
   pack(0, S);
   uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
@@ -361,6 +495,11 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       put_present();  // host copies overlap the kernel (disjoint rows of out)
       HIP_TRY(ctx, hipStreamSynchronize(s));
       return STORB_RS_OK;
+    }
+    {
+      std::vector<const uint8_t *> sin(id.begin(), id.end());
+      const int rs = streamed(ctx, k, e, coef.data(), sin.data(), od.data(), S, pack, unpack);
+      if (rs != kNotStreamed) return rs;
     }
     return sliced(ctx, S, pack, launch, unpack);
   }

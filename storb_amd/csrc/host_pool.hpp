@@ -84,9 +84,17 @@ class HostPool {
   // Measured (tools/poolbench.cpp, profiles/r3_poolbench.txt, GPU-box host):
   // one thread copies 256 KiB in 1.7 us and 1 MiB in 21 us; two threads 1 MiB
   // in 5.2 us, while 4 or 8 (waking, claiming parts) took 13-20 us; from
-  // 4 MiB on 8 threads win (28-35 us against 44 for two, 84 for one).
+  // 4 MiB on 8 threads win (28-35 us against 44 for two, 84 for one). Inside
+  // the single-chunk calls (the source hot in the caller's cache, the
+  // staging just read by the GPU) one thread packed a 512 KiB slice in
+  // 6.8 us against 13.2 with two and 13-14 with four or eight
+  // (tools/callprobe.cpp stage marks, profiles/r3m_calltrace.txt): jobs up
+  // to 1 MiB stay on the calling thread.
   int parts_for(size_t total) const {
-    if (total < (384u << 10)) return 1;
+#ifdef STORB_RS_FORCE_PARTS  // A/B builds of tools/callprobe.cpp only
+    return std::max(1, std::min(STORB_RS_FORCE_PARTS, size()));
+#endif
+    if (total <= (1u << 20)) return 1;
     if (total < (4u << 20)) return std::min(2, size());
     return static_cast<int>(std::max<size_t>(2, std::min<size_t>(size(), total / (512u << 10))));
   }

@@ -89,6 +89,30 @@ struct DescArgs {
   uint32_t cap;
 };
 
+// Streamed single call (host_calls.cpp): ONE launch over one stripe whose
+// page-locked staging the host is still filling, slice by slice, while the
+// kernel runs. A workgroup of slice s waits until ready[16 s] == seq (the
+// word the host writes once slice s is packed; the wait gives up after
+// timeout_ticks of s_memrealtime, 100 MHz, and the workgroup then exits
+// without writing), runs its tile, and the last workgroup of the slice --
+// the one that brings the device counter cnt[s] to target[s] -- writes
+// done[16 s] = seq once every store of the slice is complete. So the launch
+// latency overlaps the packing of slice 0, each slice's transfer overlaps
+// the packing of the next, and the host unpacks a slice as soon as its word
+// turns, with no launch or stream synchronisation per slice.
+constexpr int kMaxStreamSlices = 16;
+struct StreamArgs {
+  const uint32_t *ready;  // page-locked words, 64 B apart (device address)
+  uint32_t *done;         // page-locked words, 64 B apart (device address)
+  uint32_t *cnt;          // device counters, one per slice
+  uint32_t target[kMaxStreamSlices];
+  uint32_t seq;
+  uint32_t slice_cols;    // 16-B columns per slice, a multiple of the tile
+  uint32_t nslices;
+  uint32_t pad;
+  uint64_t timeout_ticks;
+};
+
 // Rows per item a mixed-row descriptor launch takes: a download's chunks
 // mostly lost 0-3 data shares (tools/descbench.cpp, bench --erase-pattern
 // download); items with more rows get launches of their own.

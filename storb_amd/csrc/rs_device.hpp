@@ -463,6 +463,85 @@ __global__ __launch_bounds__(kThreads) void rs_apply_desc_mix(const DescArgs a) 
 #undef STORB_MIX_CASE
 }
 
+// The streamed single call's kernel (StreamArgs, rs_args.h): the table
+// kernel's tile over one stripe, gated per slice on a host-written word and
+// reporting per slice through a device counter and a host-visible word. The
+// waits are bounded, so the grid always drains.
+template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR>
+__global__ __launch_bounds__(T) void rs_apply_stream(const ApplyArgs a, const StreamArgs st) {
+  constexpr uint32_t TILE = T * U;
+  const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
+  const uint32_t base = blockIdx.x * TILE;
+  const uint32_t slice = base / st.slice_cols;
+  __shared__ uint32_t go;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t ok = 1;
+    while (__hip_atomic_load(st.ready + 16 * slice, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) !=
+           st.seq) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > st.timeout_ticks) {
+        ok = 0;
+        break;
+      }
+    }
+    go = ok;
+  }
+  __syncthreads();
+  if (!go) return;
+  // the slice's staging, written by the host before its word: no stale lines
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const PermTab *tabs = a.ptab;
+  if constexpr (TL) {
+    __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * RM];
+    const uint32_t n16 = a.k * RM * (sizeof(PermTab) / 16);
+    for (uint32_t t = threadIdx.x; t < n16; t += T)
+      reinterpret_cast<u32x4 *>(lds_ptab)[t] = reinterpret_cast<const u32x4 *>(a.ptab)[t];
+    __syncthreads();
+    tabs = lds_ptab;
+  }
+  const ArgsView v{a, 0};
+  if (base + TILE <= cols)
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, false>(v, tabs, a.k, a.r, cols, base + threadIdx.x);
+  else
+    perm_tile<KM, RM, T, U, BAR, G, PAIR, true>(v, tabs, a.k, a.r, cols, base + threadIdx.x);
+  // every lane's stores complete and visible to the host before the count
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t n = __hip_atomic_fetch_add(st.cnt + slice, 1u, __ATOMIC_ACQ_REL,
+                                              __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    if (n == st.target[slice])
+      __hip_atomic_store(st.done + 16 * slice, st.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <int KM, int RM>
+hipError_t launch_stream_t(const ApplyArgs &a, const StreamArgs &st, hipStream_t s) {
+  using C = Tune<KM, RM>;
+  static_assert(C::T == kThreads && C::U == 1, "streamed calls: one tile shape");
+  const uint64_t blocks = ((a.block >> 4) + kThreads - 1) / kThreads;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((rs_apply_stream<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>),
+                     dim3(blocks), dim3(kThreads), 0, s, a, st);
+  return hipGetLastError();
+}
+
+template <int KM>
+hipError_t go_stream_r(const ApplyArgs &a, const StreamArgs &st, hipStream_t s) {
+  switch (rows_bucket(a.r)) {
+    case 1: return launch_stream_t<KM, 1>(a, st, s);
+    case 2: return launch_stream_t<KM, 2>(a, st, s);
+    case 3: return launch_stream_t<KM, 3>(a, st, s);
+    case 4: return launch_stream_t<KM, 4>(a, st, s);
+    case 5: return launch_stream_t<KM, 5>(a, st, s);
+    case 6: return launch_stream_t<KM, 6>(a, st, s);
+    case 7: return launch_stream_t<KM, 7>(a, st, s);
+    case 8: return launch_stream_t<KM, 8>(a, st, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR = false>
 hipError_t launch_perm(const ApplyArgs &a, hipStream_t s, int occ = 0, int occ_copy = 0) {
   const uint64_t cols = a.block >> 4;

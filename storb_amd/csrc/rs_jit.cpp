@@ -310,7 +310,11 @@ class Jit {
     }
   }
 
-  static void register_exit_hook() { std::atexit([] { jit().shutdown(); }); }
+  // Once per process (it was registered again after every compile).
+  static void register_exit_hook() {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit([] { jit().shutdown(); }); });
+  }
 
   // One tiny hipRTC compile in the calling thread before the first worker
   // starts (once per process, ~0.1-0.3 s): comgr builds its static state

@@ -78,15 +78,26 @@ Variant pick_variant(const storb_rs_ctx *ctx) {
 // Evict the least recently used table without blocking the host: the free
 // is ordered (on ctx->stream) after the upload and after the last launch
 // that read the table on every stream that used it.
+// Give a table's device memory back to the stream-ordered pool it came from
+// (hipMallocAsync), ordered on ctx->stream after its upload and its last
+// use on every stream. Never hipFree: that is not the pool's free (a plain
+// hipFree of pool memory was what context teardown did until round 3).
+static hipError_t release_table(storb_rs_ctx *ctx, Tables *t) {
+  if (!t->dev) return hipSuccess;
+  hipError_t e = hipStreamWaitEvent(ctx->stream, t->uploaded, 0);
+  for (auto &u : t->uses)
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, u.second, 0);
+  if (e == hipSuccess) e = hipFreeAsync(t->dev, ctx->stream);
+  if (e == hipSuccess) t->dev = nullptr;
+  return e;
+}
+
 static int evict_tables(storb_rs_ctx *ctx) {
   auto victim = ctx->tables.begin();
   for (auto it = ctx->tables.begin(); it != ctx->tables.end(); ++it)
     if (it->second->tick < victim->second->tick) victim = it;
   Tables *t = victim->second.get();
-  HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, t->uploaded, 0));
-  for (auto &u : t->uses) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, u.second, 0));
-  HIP_TRY(ctx, hipFreeAsync(t->dev, ctx->stream));
-  t->dev = nullptr;
+  HIP_TRY(ctx, release_table(ctx, t));
   // The host source of the upload must outlive the copy; that copy is the
   // oldest work on `home` this table has, long finished in practice.
   HIP_TRY(ctx, hipEventSynchronize(t->uploaded));
@@ -522,7 +533,11 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
 void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream) {
+    // tables back to their pool, after every use on any stream
+    for (auto &kv : ctx->tables) (void)release_table(ctx, kv.second.get());
+    (void)hipStreamSynchronize(ctx->stream);
+  }
   for (auto &p : ctx->pipe)
     if (p) (void)hipStreamSynchronize(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
