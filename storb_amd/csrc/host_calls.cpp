@@ -160,16 +160,19 @@ constexpr int kNotStreamed = -1;
 int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
              const uint8_t *const *in, uint8_t *const *out, size_t S,
              const std::function<void(size_t, size_t)> &pack,
-             const std::function<void(size_t, size_t)> &unpack) {
-  if (ctx->variant != STORB_RS_KERNEL_AUTO || k == 0 || k > 8 || rows == 0 || rows > 8 ||
-      S % kAlign)
+             const std::function<void(size_t, size_t)> &unpack, uint32_t enc_n = 0) {
+  if (ctx->variant != STORB_RS_KERNEL_AUTO || k == 0 || rows == 0 || S % kAlign)
     return kNotStreamed;
+  // Encode of (16, 24) / (32, 48): the bit-sliced encoder's streamed form;
+  // otherwise the table kernel's, for k <= 8 and <= 8 rows.
+  const uint32_t bs_cpt = enc_n ? bitslice_stream_cols_per_tile(k, enc_n) : 0;
+  if (!bs_cpt && (k > 8 || rows > 8)) return kNotStreamed;
+  const uint32_t cpt = bs_cpt ? bs_cpt : static_cast<uint32_t>(kThreadsTable);
   const uint32_t cols = static_cast<uint32_t>(S / 16);
   // 64 KiB of every share per slice, at most kMaxStreamSlices slices
   uint32_t slice_cols = 4096;
   if ((cols + slice_cols - 1) / slice_cols > static_cast<uint32_t>(kMaxStreamSlices))
-    slice_cols = static_cast<uint32_t>(
-        round_up((cols + kMaxStreamSlices - 1) / kMaxStreamSlices, kThreadsTable));
+    slice_cols = static_cast<uint32_t>(round_up((cols + kMaxStreamSlices - 1) / kMaxStreamSlices, cpt));
   const uint32_t nsl = (cols + slice_cols - 1) / slice_cols;
   hipStream_t s = ctx->stream;
   if (!ctx->sword_pin.p) {
@@ -182,8 +185,8 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
     std::memset(ctx->sbase, 0, sizeof(ctx->sbase));
   }
   Tables *t = nullptr;
-  int rc = get_tables(ctx, k, rows, coef, s, &t);
-  if (rc) return rc;
+  int rc;
+  if (!bs_cpt && (rc = get_tables(ctx, k, rows, coef, s, &t))) return rc;
   ApplyArgs a{};
   a.k = k;
   a.r = rows;
@@ -195,8 +198,10 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
     a.out[i] = out[i];
     a.out_stride[i] = S;
   }
-  a.ptab = reinterpret_cast<const PermTab *>(t->dev);
-  a.tab_rows = static_cast<uint32_t>(rows_bucket(rows));
+  if (t) {
+    a.ptab = reinterpret_cast<const PermTab *>(t->dev);
+    a.tab_rows = static_cast<uint32_t>(rows_bucket(rows));
+  }
   a.block = S;
   a.nstripes = 1;
   StreamArgs st{};
@@ -211,14 +216,14 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
   uint32_t tiles[kMaxStreamSlices] = {};
   for (uint32_t i = 0; i < nsl; i++) {
     const uint32_t len = std::min(slice_cols, cols - i * slice_cols);
-    tiles[i] = (len + static_cast<uint32_t>(kThreadsTable) - 1) / static_cast<uint32_t>(kThreadsTable);
+    tiles[i] = (len + cpt - 1) / cpt;
     st.target[i] = ctx->sbase[i] + tiles[i];
   }
-  const hipError_t le = launch_apply_stream(a, st, s);
+  const hipError_t le = bs_cpt ? launch_encode_bitslice_stream(a, enc_n, st, s)
+                              : launch_apply_stream(a, st, s);
   if (le == hipErrorInvalidValue) return kNotStreamed;  // nothing was queued
   HIP_TRY(ctx, le);
-  rc = tables_used(ctx, t, s);
-  if (rc) return rc;
+  if (t && (rc = tables_used(ctx, t, s))) return rc;
   uint32_t *ready_h = reinterpret_cast<uint32_t *>(ctx->sword_pin.p);
   const uint32_t *done_h = ready_h + kMaxStreamSlices * 16;
   auto range = [&](uint32_t i, size_t &off, size_t &cnt) {
@@ -366,7 +371,7 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       std::vector<const uint8_t *> sin(k);
       for (uint32_t j = 0; j < k; j++) sin[j] = dd + static_cast<size_t>(j) * S;
       const int rs = streamed(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, sin.data(),
-                              pd.data(), S, pk, up);
+                              pd.data(), S, pk, up, n);
       if (rs != kNotStreamed) return rs;
     }
     return sliced(ctx, S, pk, launch, up);

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rs_bitslice_core.h"
+#include "rs_stream.hpp"
 #include "rs_kernels.hpp"
 
 namespace storb_rs {
@@ -127,6 +128,28 @@ template <int K, int N, int CAP>
 __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(2))) void
 rs_encode_bitslice_split(const ApplyArgs a) {
   bs_split_body<EncMat<K, N>, kSplitGroup, 0>(a);
+}
+
+// The streamed single call's bit-sliced encoder (rs_stream.hpp): one stripe,
+// each workgroup gated on its tile's slice (one wave per tile geometries).
+template <int K, int N>
+__global__ __launch_bounds__((BsTune<K, N>::T)) __attribute__((amdgpu_waves_per_eu(2))) void
+rs_encode_bitslice_stream(const ApplyArgs a, const StreamArgs st) {
+  using C = BsTune<K, N>;
+  static_assert(!C::SPLIT, "streamed encode: one wave per tile");
+  const uint32_t slice = static_cast<uint32_t>(blockIdx.x * C::CPT / st.slice_cols);
+  if (!stream_gate(st, slice)) return;
+  bs_kernel_body<EncMat<K, N>, C::G, C::T, C::SWZ>(a);
+  stream_report(st, slice);
+}
+
+template <int K, int N>
+hipError_t launch_bitslice_stream(const ApplyArgs &a, const StreamArgs &st, hipStream_t s) {
+  using C = BsTune<K, N>;
+  const uint64_t blocks = ((a.block >> 4) + C::CPT - 1) / C::CPT;
+  if (blocks == 0) return hipSuccess;
+  return launch_lds<rs_encode_bitslice_stream<K, N>>(blocks, C::T, cap_lds(wg_cap(C::OCC), C::LDS),
+                                                     s, a, st);
 }
 
 template <int K, int N, int CAP>

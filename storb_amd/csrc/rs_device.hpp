@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rs_kernels.hpp"
+#include "rs_stream.hpp"
 
 namespace storb_rs {
 
@@ -473,24 +474,7 @@ __global__ __launch_bounds__(T) void rs_apply_stream(const ApplyArgs a, const St
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t base = blockIdx.x * TILE;
   const uint32_t slice = base / st.slice_cols;
-  __shared__ uint32_t go;
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t ok = 1;
-    while (__hip_atomic_load(st.ready + 16 * slice, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) !=
-           st.seq) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > st.timeout_ticks) {
-        ok = 0;
-        break;
-      }
-    }
-    go = ok;
-  }
-  __syncthreads();
-  if (!go) return;
-  // the slice's staging, written by the host before its word: no stale lines
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (!stream_gate(st, slice)) return;
   const PermTab *tabs = a.ptab;
   if constexpr (TL) {
     __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * RM];
@@ -505,15 +489,7 @@ __global__ __launch_bounds__(T) void rs_apply_stream(const ApplyArgs a, const St
     perm_tile<KM, RM, T, U, BAR, G, PAIR, false>(v, tabs, a.k, a.r, cols, base + threadIdx.x);
   else
     perm_tile<KM, RM, T, U, BAR, G, PAIR, true>(v, tabs, a.k, a.r, cols, base + threadIdx.x);
-  // every lane's stores complete and visible to the host before the count
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t n = __hip_atomic_fetch_add(st.cnt + slice, 1u, __ATOMIC_ACQ_REL,
-                                              __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    if (n == st.target[slice])
-      __hip_atomic_store(st.done + 16 * slice, st.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  stream_report(st, slice);
 }
 
 template <int KM, int RM>

@@ -46,9 +46,9 @@ inline size_t cap_lds(int cap, size_t static_lds) {
 #ifdef __HIPCC__
 // Launch kernel Kern with `dyn` bytes of dynamic LDS (the resident-workgroup
 // cap); above 64 KiB each kernel must opt in once.
-template <auto Kern, class Args>
+template <auto Kern, class... Args>
 hipError_t launch_lds(uint64_t blocks, int threads, size_t dyn, hipStream_t s,
-                      const Args &a) {
+                      const Args &...a) {
   if (dyn > (64u << 10)) {
     static std::atomic<size_t> opted{0};  // per kernel instantiation
     if (opted.load(std::memory_order_relaxed) < dyn) {
@@ -59,7 +59,7 @@ hipError_t launch_lds(uint64_t blocks, int threads, size_t dyn, hipStream_t s,
       opted.store(dyn, std::memory_order_relaxed);
     }
   }
-  hipLaunchKernelGGL(Kern, dim3(blocks), dim3(threads), dyn, s, a);
+  hipLaunchKernelGGL(Kern, dim3(blocks), dim3(threads), dyn, s, a...);
   return hipGetLastError();
 }
 #endif
@@ -90,6 +90,11 @@ hipError_t launch_apply_desc(const DescArgs &a, hipStream_t s);
 // n - k parity slots; needs vector_ok(a).
 bool bitslice_supported(uint32_t k, uint32_t n);
 hipError_t launch_encode_bitslice(const ApplyArgs &a, uint32_t n, hipStream_t s);
+// Streamed single-call form (StreamArgs): (16, 24) and (32, 48); columns per
+// workgroup tile (0: no streamed encoder for the geometry).
+uint32_t bitslice_stream_cols_per_tile(uint32_t k, uint32_t n);
+hipError_t launch_encode_bitslice_stream(const ApplyArgs &a, uint32_t n, const StreamArgs &st,
+                                         hipStream_t s);
 
 hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
                                uint64_t stride, uint8_t *out, hipStream_t s);
