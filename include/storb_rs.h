@@ -179,8 +179,10 @@ int storb_rs_decode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
  * so the survivor set varies from chunk to chunk. Stripe s offers nshares[s]
  * shares, share_idx[o_s .. o_s + nshares[s]) with o_s = nshares[0] + ... +
  * nshares[s-1]. Layout and d_out semantics as storb_rs_decode_batch_dev.
- * One launch per missing-row count over all stripes (each workgroup reads its
- * own stripe's pattern), not one per pattern. ENOTENOUGH names the stripe. */
+ * One launch over every stripe that lost up to 4 data shares (each workgroup
+ * reads its own stripe's pattern and runs the tile of its own row count),
+ * plus one per larger missing-row count -- never one per pattern.
+ * ENOTENOUGH names the stripe. */
 int storb_rs_decode_stripes_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                                 size_t block, uint32_t nstripes,
                                 const uint32_t *share_idx, const uint32_t *nshares,
