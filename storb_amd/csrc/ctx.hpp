@@ -190,6 +190,8 @@ struct storb_rs_ctx {
   storb_rs::detail::PinBuf desc_pin[storb_rs::detail::kDescRing];
   storb_rs::detail::DevBuf desc_dev[storb_rs::detail::kDescRing];
   hipEvent_t desc_ev[storb_rs::detail::kDescRing] = {};
+  hipStream_t desc_stream = nullptr;  // the descriptor copies
+  hipEvent_t desc_copied = nullptr;
   unsigned desc_next = 0;
   // Slots of the asynchronous host calls (host_async.cpp); async_mu guards
   // the busy flags, which finish() clears without holding mu.

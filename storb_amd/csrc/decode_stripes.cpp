@@ -165,7 +165,16 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
   }
   uint8_t *dev = ctx->desc_dev[slot].p, *hd = nullptr;
   HIP_TRY(ctx, host_dev_ptr(h, &hd));
-  hipError_t e = launch_copy16(dev, hd, total, s);
+  // The copy runs on the context's descriptor stream, so it overlaps whatever
+  // the caller's stream is still running (the slot is free: its last use has
+  // completed); the decode launches wait for it on the device.
+  if (!ctx->desc_stream) {
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->desc_stream, hipStreamNonBlocking));
+    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_copied, hipEventDisableTiming));
+  }
+  hipError_t e = launch_copy16(dev, hd, total, ctx->desc_stream);
+  if (e == hipSuccess) e = hipEventRecord(ctx->desc_copied, ctx->desc_stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, ctx->desc_copied, 0);
   for (size_t gi = 0; e == hipSuccess && gi < groups.size(); gi++) {
     const Group &g = *groups[gi];
     DescArgs a{};

@@ -545,6 +545,11 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->desc_stream) {
+    (void)hipStreamSynchronize(ctx->desc_stream);
+    (void)hipStreamDestroy(ctx->desc_stream);
+    (void)hipEventDestroy(ctx->desc_copied);
+  }
   for (auto &e : ctx->desc_ev)  // descriptor launches may run on callers' streams
     if (e) {
       (void)hipEventSynchronize(e);

@@ -200,6 +200,39 @@ def test_single_call_large_ragged(ctx, k, n, L):
         assert got == data.tobytes(), (k, n, L, lost)
 
 
+@pytest.mark.parametrize("k,n", [(2, 3), (3, 5), (4, 6), (8, 12), (16, 24), (32, 48)])
+def test_single_call_streamed_slices(ctx, k, n):
+    """The streamed single calls (host_calls.cpp streamed: one launch gated
+    per 64 KiB-per-share slice on host-written words; the table kernel for
+    k <= 8, the bit-sliced encoders for (16, 24) / (32, 48)) from pageable
+    buffers, at lengths that put the slice edges, the zero padding and the
+    truncated last row everywhere: one slice, exact slice multiples, one byte
+    over, a ragged 16-B column count, and more than 16 slices (the slice
+    grows). Every call is oracle-exact, and the calls are repeated so the
+    per-slice counters run across geometries and slice counts."""
+    rng = random.Random(k * 100 + n)
+    S64 = 64 << 10
+    lengths = [1000, k * S64, k * S64 + 1, k * (3 * S64 + 4096 + 48) - 7, k * 20 * S64 + 333]
+    if k >= 16:
+        lengths = [1000, k * S64, k * (3 * S64 + 48) - 7, k * 18 * S64 + 5]
+    for rep in range(2):
+        for L in lengths:
+            data = rnd(L, L + rep)
+            par, B, pad = ctx.encode(k, n, data)
+            want, wB, wpad = oracle_parity(k, n, data)
+            assert (B, pad) == (wB, wpad)
+            for i in range(n - k):
+                assert par[i] == want[i].tobytes(), (k, n, L, i)
+            if k > 8:  # decode of k > 8 is not streamed; encode is
+                continue
+            shares = coracle.encode(k, n, data)[0]
+            lost = rng.sample(range(k), rng.randint(1, min(n - k, k)))
+            ids = [i for i in range(n) if i not in lost]
+            rng.shuffle(ids)
+            got = ctx.decode(k, n, [shares[i] for i in ids], ids, B, pad)
+            assert got == data.tobytes(), (k, n, L, lost)
+
+
 def test_host_decode_chunks_batch(ctx):
     """Batched download-side decode: every chunk its own survivor set
     (all-data, data+parity mixes, parity-only, extra shares beyond k, any

@@ -187,36 +187,7 @@ def test_decode_chunks_download_patterns(k, n, B, cnt, where):
 def test_decode_chunks_each_chunk_in_its_own_registered_buffer():
     """shares of consecutive chunks in separate registered ranges
     at equal spacing -- a device address is taken per range, never derived
-    from another chunk's mapping. Oracle-exact."""
-    c = _lib.Context(0)
-    k, n, B, cnt = 4, 6, 64 << 10, 8
-    data, par = oracle_stripes(k, n, B, cnt, 99)
-    # one host allocation, one registered range per chunk (equal spacing)
-    span = n * B + 4096
-    host = np.zeros(cnt * span + 4096, np.uint8)
-    base = (-host.ctypes.data) % 4096
-    regs = []
-    try:
-        for ch in range(cnt):
-            seg = host[base + ch * span: base + ch * span + n * B]
-            seg[:k * B] = data[ch].reshape(-1)
-            seg[k * B:] = par[ch].reshape(-1)
-            rc = _lib.lib().storb_rs_host_register(seg.ctypes.data, seg.nbytes)
-            assert rc == 0
-            regs.append(seg)
-        out_buf = _lib.PinnedBuffer(cnt * k * B)
-        out = out_buf.array.reshape(cnt, k * B)
-        rng = random.Random(3)
-        chunks = []
-        for ch in range(cnt):
-            lost = rng.sample(range(k), 2)
-            ids = [i for i in range(n) if i not in lost]
-            chunks.append(([regs[ch][i * B:(i + 1) * B] for i in ids], ids))
-        got = c.decode_chunks(k, n, B, 0, chunks, out=out)
-        for ch in range(cnt):
-            assert np.array_equal(got[ch], data[ch].reshape(-1)), ch
-        out_buf.free()
-    finally:
-        for seg in regs:
-            _lib.lib().storb_rs_host_unregister(seg.ctypes.data)
-        c.close()
+    from another chunk's mapping. Oracle-exact; runs in a child process
+    (tests/registered_ranges.py)."""
+    from test_gpu_runtime import run_registered_case
+    run_registered_case("each_chunk_own_range")

@@ -9,6 +9,7 @@
   place by the zero-copy paths (interior offsets), matching the oracle.
 """
 import itertools
+import os
 import random
 
 import numpy as np
@@ -21,6 +22,17 @@ from storb_amd import _lib
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
+
+
+def run_registered_case(case):
+    """tests/registered_ranges.py CASE in a child process (see its docstring)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "registered_ranges.py"), case],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and f"{case} ok" in r.stdout, (r.returncode, r.stdout[-2000:],
+                                                          r.stderr[-4000:])
 
 
 def rnd(n, seed):
@@ -128,42 +140,8 @@ def page_aligned(nbytes, align=4096):
     return raw, raw[off:off + nbytes]
 
 
-def test_host_register_direct_paths(ctx):
+def test_host_register_direct_paths():
     """storb_rs_host_register'd caller memory (mapped) used in place at
-    interior offsets by encode, decode and encode_chunks; oracle-exact."""
-    k, n, B = 4, 6, 64 << 10
-    L = k * B
-    raw, buf = page_aligned(16 << 20)
-    base = buf.ctypes.data
-    lib = _lib.lib()
-    assert lib.storb_rs_host_register(base, buf.nbytes) == _lib.OK
-    try:
-        assert _lib.host_is_pinned(buf[4096:4096 + L])
-        data = buf[4096:4096 + L]                  # interior, 16-B aligned
-        data[:] = rnd(L, 11)
-        want, _, _ = coracle.encode(k, n, data)
-        parity = [buf[(1 << 20) + i * B:(1 << 20) + (i + 1) * B] for i in range(n - k)]
-        ctx.encode_into(k, n, data, parity)
-        for i in range(n - k):
-            assert np.array_equal(parity[i], want[k + i]), i
-        # decode: survivors {1, 3, 4, 5} from registered memory into registered out
-        surv = [1, 3, 4, 5]
-        sh = [buf[(2 << 20) + j * B:(2 << 20) + (j + 1) * B] for j in range(len(surv))]
-        for j, s in enumerate(surv):
-            sh[j][:] = want[s]
-        out = buf[(3 << 20):(3 << 20) + L]
-        out[:] = 0
-        ctx.decode_into(k, n, sh, surv, B, 0, out)
-        assert np.array_equal(out, data)
-        # batch encode: chunks and parity both registered
-        nch, cl = 6, 512 << 10
-        chunks = buf[(4 << 20):(4 << 20) + nch * cl]
-        chunks[:] = rnd(nch * cl, 12)
-        pout = buf[(8 << 20):(8 << 20) + nch * (n - k) * (cl // k)]
-        ctx.encode_chunks(k, n, chunks, cl, nch, out=pout)
-        want_p = coracle.encode_parity_many(k, n, chunks, cl, nch)
-        assert np.array_equal(pout, want_p)
-    finally:
-        assert lib.storb_rs_host_unregister(base) == _lib.OK
-    assert not _lib.host_is_pinned(buf[4096:4096 + L])
-    del raw
+    interior offsets by encode, decode and encode_chunks; oracle-exact. Runs
+    in a child process (tests/registered_ranges.py)."""
+    run_registered_case("direct_paths")
