@@ -87,7 +87,8 @@ def main():
         if ci % 2000 == 1000 and st["pending"]:
             during.append(host_rate(ctx, k, n, B, hn, hs, hdata))
         if ci % 1000 == 0:
-            print(json.dumps({"call": ci, "bad": bad, **st}), flush=True)
+            print(json.dumps({"call": ci, "t": round(time.perf_counter() - t0, 2), "bad": bad, **st}),
+                  flush=True)
     torch.cuda.synchronize()
     _lib.jit_wait()
     st = _lib.jit_stats()

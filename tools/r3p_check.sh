@@ -5,7 +5,7 @@
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r3p; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_piece_api.py tests/test_gpu_async.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_piece_api.py tests/test_gpu_async.py tests/test_gpu_runtime.py tests/test_gpu_patterns.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 timeout -k 10 200 python -u tools/fuzz.py --seconds 60 --seed 47 > $O/fuzz.json 2>&1 || { echo "fuzz failed"; tail -20 $O/fuzz.json; exit 1; }
 tail -1 $O/fuzz.json
