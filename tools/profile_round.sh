@@ -19,6 +19,9 @@ trace() {  # name, bench args...
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$name" \
     -o run -- python3 bench.py --no-host-path --no-traffic --cpu-seconds 0 "$@" \
     > "$OUT/bench_$name.log" 2>&1
+  # keep the --stats summary (what profiles/summarize.py reads); the full
+  # per-dispatch trace would push gpurun_out past its copy-back limit
+  find "$OUT/trace_$name" -name "*kernel_trace.csv" -delete
   echo "traced $name"
 }
 trace config2
