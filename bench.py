@@ -1086,7 +1086,10 @@ def main():
                               "separate untimed pass with an event after every leg"),
             "alg_bytes_per_launch": alg,
             "kernel_match": {leg: leg_kernel_match(a, w, leg) for leg in w.legs},
-            "launches_per_leg": {leg: (len({len(x) for x in w.lost if x})
+            # download patterns: one mixed-row launch for the stripes that lost
+            # 1-4 data shares, one per larger count (decode_stripes.cpp)
+            "launches_per_leg": {leg: ((1 if any(0 < len(x) <= 4 for x in w.lost) else 0) +
+                                       len({len(x) for x in w.lost if len(x) > 4})
                                        if leg == "decode" and w.sets is not None
                                        else jit_blocks(w.k, leg_rows(w, leg))[0]
                                        if leg in w.jit_legs else 1) for leg in w.legs},
