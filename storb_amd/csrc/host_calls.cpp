@@ -326,7 +326,7 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       size_t avail = off < B ? std::min(cnt, B - off) : 0;
       avail = src < len ? std::min(avail, len - src) : 0;
       uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(j) * S + off;
-      if (avail) segs.push_back({dst, data + src, avail, true});
+      if (avail) segs.push_back({dst, data + src, avail});
       if (cnt > avail) segs.push_back({dst + avail, nullptr, cnt - avail});
     }
     pool.copy_segs(segs.data(), segs.size());
@@ -453,7 +453,7 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       const size_t avail = off < block ? std::min(cnt, block - off) : 0;
       if (!in_direct) {
         uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(c) * S + off;
-        if (avail) segs.push_back({dst, src, avail, true});
+        if (avail) segs.push_back({dst, src, avail});
         if (cnt > avail) segs.push_back({dst + avail, nullptr, cnt - avail});
       }
       if (slot_idx[c] < k) put_cols(c, off, cnt, src);

@@ -18,62 +18,17 @@
 #include <thread>
 #include <vector>
 
-#if defined(__x86_64__)
-#include <immintrin.h>
-#endif
-
 namespace storb_rs {
 
-// A byte range to copy (src != nullptr) or to zero-fill (src == nullptr);
-// nt: the destination is page-locked staging only the GPU reads next, so
-// the copy may bypass the CPU caches (copy_stream).
+// A byte range to copy (src != nullptr) or to zero-fill (src == nullptr).
+// (Non-temporal stores for the copies into staging were measured and not
+// kept: equal at 1 MiB calls, slower at 8 MiB -- (16, 24) encode 315 ->
+// 380 us -- tools/callprobe.cpp, profiles/r3u_copy_split_nt_ab.txt.)
 struct CopySeg {
   uint8_t *dst;
   const uint8_t *src;
   size_t len;
-  bool nt = false;
 };
-
-#if defined(__x86_64__)
-// memcpy with non-temporal 32-byte stores: no read-for-ownership of the
-// destination lines and no cache pollution -- for the single calls' packing
-// of pageable chunks into the staging the streamed kernel reads over PCIe.
-// Ends with sfence (the stores are weakly ordered; the caller publishes the
-// slice after this returns).
-__attribute__((target("avx2"))) inline void copy_stream_avx2(uint8_t *d, const uint8_t *s,
-                                                              size_t n) {
-  size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
-  if (head > n) head = n;
-  std::memcpy(d, s, head);
-  d += head;
-  s += head;
-  n -= head;
-  size_t i = 0;
-  for (; i + 128 <= n; i += 128) {
-    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
-    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 32));
-    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 64));
-    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 96));
-    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), a);
-    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 32), b);
-    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 64), c);
-    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 96), e);
-  }
-  std::memcpy(d + i, s + i, n - i);
-  _mm_sfence();
-}
-#endif
-
-inline void copy_stream(uint8_t *d, const uint8_t *s, size_t n) {
-#if defined(__x86_64__) && !defined(STORB_RS_NO_NT_PACK)
-  static const bool avx2 = __builtin_cpu_supports("avx2");
-  if (avx2 && n >= 4096) {
-    copy_stream_avx2(d, s, n);
-    return;
-  }
-#endif
-  std::memcpy(d, s, n);
-}
 
 class HostPool {
  public:
@@ -162,9 +117,8 @@ class HostPool {
         const CopySeg &sg = segs[i];
         if (base + sg.len > lo) {
           const size_t a = lo - base, b = std::min(sg.len, hi - base);
-          if (!sg.src) std::memset(sg.dst + a, 0, b - a);
-          else if (sg.nt) copy_stream(sg.dst + a, sg.src + a, b - a);
-          else std::memcpy(sg.dst + a, sg.src + a, b - a);
+          if (sg.src) std::memcpy(sg.dst + a, sg.src + a, b - a);
+          else std::memset(sg.dst + a, 0, b - a);
           lo = base + b;
         }
         base += sg.len;
