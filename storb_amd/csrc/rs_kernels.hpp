@@ -99,7 +99,7 @@ hipError_t launch_encode_bitslice_stream(const ApplyArgs &a, uint32_t n, const S
 hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
                                uint64_t stride, uint8_t *out, hipStream_t s);
 
-// The streamed single-call kernel (rs_stream.hip): k <= 8, 1 <= r <= 8,
+// The streamed single-call kernel (rs_stream.hip): k <= 32, 1 <= r <= 8,
 // one stripe, dwordx4-aligned slots; hipErrorInvalidValue otherwise.
 hipError_t launch_apply_stream(const ApplyArgs &a, const StreamArgs &st, hipStream_t s);
 // dst (device) <- src (device-accessible, e.g. page-locked host), 16-B

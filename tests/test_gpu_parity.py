@@ -204,7 +204,7 @@ def test_single_call_large_ragged(ctx, k, n, L):
 def test_single_call_streamed_slices(ctx, k, n):
     """The streamed single calls (host_calls.cpp streamed: one launch gated
     per 64 KiB-per-share slice on host-written words; the table kernel for
-    k <= 8, the bit-sliced encoders for (16, 24) / (32, 48)) from pageable
+    k <= 32 and <= 8 rows, the bit-sliced encoders for (16, 24) / (32, 48)) from pageable
     buffers, at lengths that put the slice edges, the zero padding and the
     truncated last row everywhere: one slice, exact slice multiples, one byte
     over, a ragged 16-B column count, and more than 16 slices (the slice
@@ -223,10 +223,8 @@ def test_single_call_streamed_slices(ctx, k, n):
             assert (B, pad) == (wB, wpad)
             for i in range(n - k):
                 assert par[i] == want[i].tobytes(), (k, n, L, i)
-            if k > 8:  # decode of k > 8 is not streamed; encode is
-                continue
             shares = coracle.encode(k, n, data)[0]
-            lost = rng.sample(range(k), rng.randint(1, min(n - k, k)))
+            lost = rng.sample(range(k), rng.randint(1, min(n - k, k, 8)))
             ids = [i for i in range(n) if i not in lost]
             rng.shuffle(ids)
             got = ctx.decode(k, n, [shares[i] for i in ids], ids, B, pad)
