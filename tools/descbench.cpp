@@ -16,6 +16,9 @@
 // build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/descbench.cpp -Iinclude \
 //   -Istorb_amd/csrc -Lstorb_amd/lib -lstorb_rs -Wl,-rpath,'$ORIGIN/../../storb_amd/lib' \
 //   -o tools/_build/descbench
+// usage: descbench [REPS] [K]; K = 32 runs config 6's download shape instead
+// (32 chunks x 32 MiB, k = 32, n = 48, B = 1 MiB; 4 / 14 / 13 / 1 chunks lost
+// 0 / 1 / 2 / 3 data shares, the histogram of profiles/r3k_bench_c6_download.json).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,8 +44,10 @@ using namespace storb_rs;
 
 int main(int argc, char **argv) {
   const int reps = argc > 1 ? std::atoi(argv[1]) : 20;
-  const uint32_t k = 16, n = 24, N = 128;
-  const size_t B = 512u << 10;
+  const bool c6 = argc > 2 && std::atoi(argv[2]) == 32;
+  const uint32_t k = c6 ? 32 : 16, n = k + k / 2, N = c6 ? 32 : 128;
+  const size_t B = c6 ? (1u << 20) : (512u << 10);
+  const int hist[4] = {c6 ? 4 : 13, c6 ? 14 : 48, c6 ? 13 : 58, c6 ? 1 : 9};
   uint8_t *d = nullptr, *p = nullptr;
   CK(hipMalloc(&d, N * k * B));
   CK(hipMalloc(&p, N * (n - k) * B));
@@ -50,10 +55,8 @@ int main(int argc, char **argv) {
   CK(hipMemset(p, 0x5A, N * (n - k) * B));
   std::mt19937 rng(5);
   std::vector<uint32_t> es;
-  for (int i = 0; i < 13; i++) es.push_back(0);
-  for (int i = 0; i < 48; i++) es.push_back(1);
-  for (int i = 0; i < 58; i++) es.push_back(2);
-  for (int i = 0; i < 9; i++) es.push_back(3);
+  for (uint32_t e = 0; e < 4; e++)
+    for (int i = 0; i < hist[e]; i++) es.push_back(e);
   std::shuffle(es.begin(), es.end(), rng);
   // per stripe: survivors (first k of the shares not lost) and lost rows
   std::vector<std::vector<uint32_t>> surv(N), lost(N);
@@ -191,7 +194,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&dmtab, mtab.size() * sizeof(PermTab)));
   CK(hipMemcpy(dmrec, mrec.data(), mrec.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dmtab, mtab.data(), mtab.size() * sizeof(PermTab), hipMemcpyHostToDevice));
-  for (uint32_t cap : {0u, 2u, 3u, 4u, 8u}) {
+  for (uint32_t cap : {0u, 2u, 3u, 4u, 6u, 8u}) {
     for (uint32_t tpw : {1u, 2u}) {
       DescArgs a{};
       a.desc = dmrec;
@@ -200,7 +203,7 @@ int main(int argc, char **argv) {
       a.k = k;
       a.r = kMixR;
       a.tpw = tpw;
-      a.nitems = N - 13;
+      a.nitems = N - hist[0];
       a.rec_qwords = 1 + k + kMixR;
       a.mix = 1;
       a.cap = cap;
@@ -228,7 +231,9 @@ int main(int argc, char **argv) {
   storb_rs_set_kernel(ctx, STORB_RS_KERNEL_PERM);
   std::vector<uint32_t> s2;
   for (uint32_t i = 2; i < n && s2.size() < k; i++) s2.push_back(i);
-  if (timeit("uniform: 128 stripes, 2 lost, rs_apply_perm<16,2>", [&] {
+  char uname[96];
+  std::snprintf(uname, sizeof(uname), "uniform: %u stripes, 2 lost, rs_apply_perm<%u,2>", N, k);
+  if (timeit(uname, [&] {
         storb_rs_decode_batch_dev(ctx, k, n, B, N, s2.data(), k, d, 0, p, 0, d, 0, st[0]);
       }, double(N) * (k + 2) * B))
     return 1;
