@@ -110,6 +110,49 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+def _cpu_where(cpu):
+    """Clock and NUMA node of logical CPU `cpu` (from /proc and /sys)."""
+    mhz, node = None, None
+    try:
+        cur = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("processor"):
+                cur = int(line.split(":")[1])
+            elif line.startswith("cpu MHz") and cur == cpu:
+                mhz = float(line.split(":")[1])
+                break
+    except (OSError, ValueError):
+        pass
+    try:
+        for name in os.listdir(f"/sys/devices/system/cpu/cpu{cpu}"):
+            if name.startswith("node") and name[4:].isdigit():
+                node = int(name[4:])
+    except OSError:
+        pass
+    return {"cpu": cpu, "cpu_mhz": mhz, "numa_node": node}
+
+
+def _proc_stat():
+    """Per-CPU jiffies from /proc/stat: {cpu: (total, steal)}."""
+    out = {}
+    try:
+        for line in open("/proc/stat"):
+            if line.startswith("cpu") and line[3:4].isdigit():
+                f = line.split()
+                v = [int(x) for x in f[1:]]
+                out[int(f[0][3:])] = (sum(v), v[7] if len(v) > 7 else 0)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _steal_frac(st0, st1, cpu):
+    if cpu not in st0 or cpu not in st1:
+        return None
+    tot = st1[cpu][0] - st0[cpu][0]
+    return round((st1[cpu][1] - st0[cpu][1]) / tot, 4) if tot > 0 else None
+
+
 def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=True,
                  survivor_sets=None):
     """Reference CPU path (C restatement of zfec, oracle/) on this host.
@@ -117,49 +160,58 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
     Single thread, like the reference: upload.rs:418-420 encodes one object's
     chunks sequentially in one task and download.rs:505-529 decodes them
     sequentially. Sample: 8 distinct splitmix chunks of the benchmark's
-    shape, cycled until `seconds` of CPU time are spent.
+    shape, cycled for `seconds` in a C loop on this thread
+    (oracle/cpu_bench.c). `value`: every call allocates its outputs as
+    zfec-rs does (a Vec per share, a Vec out -- piece.rs:329,384-386);
+    `arithmetic_only`: the same loop with every buffer allocated once. Both
+    carry the thread's own getrusage account (user / system seconds, minor
+    faults, context switches) and the CPU, clock and NUMA node it ran on, so
+    a figure that moves between boxes shows where.
     """
     from oracle import coracle  # test infrastructure: the baseline, never the product
 
     survivors = [i for i in range(n) if i not in erased][:k]
     sets = [sorted(x)[:k] for x in survivor_sets] if survivor_sets else [survivors]
-    sample = [coracle.splitmix_bytes(SEED_BASE + i, chunk_bytes) for i in range(8)]
-    prepared = [coracle.encode(k, n, d) for d in sample]
-    done = 0
-    t0 = time.perf_counter()
-    c0 = time.thread_time()
-    while True:
-        i = done % len(sample)
-        if do_encode:
-            shares, B, pad = coracle.encode(k, n, sample[i])
-        else:
-            shares, B, pad = prepared[i]
-        if do_decode:
-            sv = sets[done % len(sets)]
-            rec = coracle.decode(k, n, [shares[s] for s in sv], sv, B, pad)
-            if done < len(sample) and rec != sample[i].tobytes():
-                raise SystemExit("CPU baseline round trip failed")
-        done += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    el = time.perf_counter() - t0
-    on_cpu = time.thread_time() - c0
+    sample = np.concatenate([coracle.splitmix_bytes(SEED_BASE + i, chunk_bytes)
+                             for i in range(8)])
     legs = int(do_encode) + int(do_decode)
     what = "+".join(x for x, on in (("encode", do_encode), ("decode", do_decode)) if on)
+
+    def run(fresh, secs):
+        st0 = _proc_stat()
+        r = coracle.bench_roundtrip(k, n, sample, chunk_bytes, 8, sets, do_encode, do_decode,
+                                    fresh, secs)
+        st1 = _proc_stat()
+        el = r["wall_s"]
+        acct = {"user_s": round(r["user_s"], 3), "sys_s": round(r["sys_s"], 3),
+                "thread_cpu_over_wall": round((r["user_s"] + r["sys_s"]) / el, 3),
+                "minor_faults": r["minflt"], "major_faults": r["majflt"],
+                "minor_faults_per_call": round(r["minflt"] / max(1, r["calls"]), 2),
+                "voluntary_switches": r["nvcsw"], "involuntary_switches": r["nivcsw"],
+                **_cpu_where(r["cpu_start"]),
+                # time the hypervisor ran something else on this vCPU: the
+                # thread's own CPU time does not show it (/proc/stat steal)
+                "cpu_steal_frac": _steal_frac(st0, st1, r["cpu_start"])}
+        if r["cpu_end"] != r["cpu_start"]:
+            acct["cpu_end"] = r["cpu_end"]
+        return round(legs * r["calls"] * chunk_bytes / GIB / el, 4), r["calls"], el, acct
+
+    value, calls, el, acct = run(True, seconds)
+    arith, acalls, ael, aacct = run(False, max(1.0, seconds / 2))
+    shape = (f"{chunk_bytes >> 10} KiB chunks (k={k},n={n}"
+             f"{', erased ' + (str(sorted(erased)) if not survivor_sets else 'per chunk (download patterns)') if do_decode else ''})")
     return {
-        "value": round(legs * done * chunk_bytes / GIB / el, 4),
+        "value": value,
         "unit": "GiB/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"{done} x {what} of {chunk_bytes >> 10} KiB chunks (k={k},n={n}"
-                   f"{', erased ' + (str(sorted(erased)) if not survivor_sets else 'per chunk (download patterns)') if do_decode else ''}), {el:.1f} s, "
-                   f"1 thread, scalar table-driven zfec restatement -O2 (oracle/); host "
+        "sample": (f"{calls} x {what} of {shape}, {el:.1f} s, 1 thread, scalar table-driven "
+                   f"zfec restatement -O2 (oracle/), per-call allocation as zfec-rs; host "
                    f"{platform.machine()}, {os.cpu_count()} logical CPUs visible"),
-        # CPU time the measuring thread got over the wall time of the sample:
-        # well below 1 means the host descheduled it (the GPU boxes are shared;
-        # the same binary has measured 0.11 and 1.9 GiB/s on different boxes,
-        # DESIGN.md §5)
-        "thread_cpu_over_wall": round(on_cpu / el, 3),
+        "thread": acct,
+        "arithmetic_only": {"value": arith, "unit": "GiB/s",
+                            "sample": f"{acalls} x {what}, {ael:.1f} s, buffers allocated once",
+                            "thread": aacct},
     }
 
 
@@ -366,7 +418,9 @@ def shim_path_rate(ctx, seconds=0.4):
     (upload.rs:209 chunking, piece.rs:307-317 k and m). Two figures per call:
     `call` = the C call alone on pageable caller buffers; `shim` = what
     lib.rs does around it too (m fresh zeroed Vecs, the k data shares copied
-    out of the chunk; decode: a fresh output Vec). Median per-call latency;
+    out of the chunk -- since round 4 one storb_rs_encode_shares call into
+    m unzeroed Vecs, the data shares copied by the library during the
+    kernel; decode: a fresh output Vec). Median per-call latency;
     decode loses data shares 0.. (2 at most) and gets the first k survivors
     by index, as decode_chunk hands them over (piece.rs:368-381)."""
     L = _lib.lib()
@@ -394,14 +448,15 @@ def shim_path_rate(ctx, seconds=0.4):
                 raise SystemExit(f"shim_path: storb_rs_encode rc {rc}")
 
         def enc_shim():
-            shares = [np.zeros(B, np.uint8) for _ in range(n)]  # vec![0u8; b] x m
-            for j in range(k):
-                shares[j][:B] = data[j * B:(j + 1) * B]
-            ptr = (_lib.vp * (n - k))(*[shares[i].ctypes.data for i in range(k, n)])
-            rc = L.storb_rs_encode(ctx.handle, k, n, data.ctypes.data, chunk, ptr,
-                                   _lib.C.byref(bo), _lib.C.byref(po))
+            # lib.rs Fec::encode: m Vecs with capacity b (not zero-filled), all
+            # m shares written by one storb_rs_encode_shares call (the data
+            # shares copied by the library's host pool during the kernel)
+            shares = [np.empty(B, np.uint8) for _ in range(n)]
+            ptr = (_lib.vp * n)(*[x.ctypes.data for x in shares])
+            rc = L.storb_rs_encode_shares(ctx.handle, k, n, data.ctypes.data, chunk, ptr,
+                                          _lib.C.byref(bo), _lib.C.byref(po))
             if rc:
-                raise SystemExit(f"shim_path: storb_rs_encode rc {rc}")
+                raise SystemExit(f"shim_path: storb_rs_encode_shares rc {rc}")
 
         enc_call()
         allsh = [data[j * B:(j + 1) * B].copy() for j in range(k)] + [x.copy() for x in par]
@@ -416,7 +471,7 @@ def shim_path_rate(ctx, seconds=0.4):
                 raise SystemExit(f"shim_path: storb_rs_decode rc {rc}")
 
         def dec_shim():
-            o = np.zeros(k * B, np.uint8)  # vec![0u8; k*b - padding]
+            o = np.empty(k * B, np.uint8)  # Vec::with_capacity(k*b - padding), filled by the call
             rc = L.storb_rs_decode(ctx.handle, k, n, sp_, ids, k, B, 0, o.ctypes.data)
             if rc:
                 raise SystemExit(f"shim_path: storb_rs_decode rc {rc}")
@@ -441,7 +496,10 @@ def shim_path_rate(ctx, seconds=0.4):
                          "thread_cpu_over_wall": round((time.thread_time() - c0) / wall, 3)}
         rows.append(row)
     res["geometries"] = rows
-    res["sdma_ceiling_GiBps_user"] = 35.5
+    # Not measured here: the box's SDMA PCIe ceiling in user bytes of RS(4,2)
+    # encode (57 GB/s both directions / 1.5 bytes per user byte), cited from
+    # tools/pcie_probe.py's run, profiles/r1_pcie_probe.jsonl.
+    res["cited_sdma_ceiling_GiBps_user"] = {"value": 35.5, "source": "profiles/r1_pcie_probe.jsonl"}
     return res
 
 
@@ -469,6 +527,83 @@ def shard_hash_rate(ctx, w, stream, reps=3):
     return {"value": round(nbytes / (ms * 1e-3) / 1e9, 1), "unit": "GB/s of shard bytes",
             "ms": round(ms, 4), "shards": w.N * w.n, "shard_bytes": w.B,
             "what": "blake3 (Storb piece id) of all data+parity shards, batched kernel"}
+
+
+def download_sets(k, n, nchunks, seed, fail=0.0):
+    """Per-chunk survivor sets as Storb's download collects them: the first
+    k + 1 pieces to arrive from 10 fetch threads (download.rs:363-451,
+    storb_amd/objects.py download_arrivals); decode_chunk then sorts and
+    takes the first k (piece.rs:368-381)."""
+    from storb_amd import objects
+    rng = np.random.default_rng(seed)
+    sets = []
+    while len(sets) < nchunks:
+        fail_set = {i for i in range(n) if rng.random() < fail} if fail > 0 else ()
+        got = objects.download_arrivals(k, n, rng, fail=fail_set)
+        if len(got) >= k:
+            sets.append(got)
+    return sets
+
+
+def download_leg(ctx, w, stream, a, reps=20):
+    """Storb's real download decode, device-resident, beside the headline
+    (outside its timed region): the batch's chunks each keep their own
+    survivor set (download_sets), and one storb_rs_decode_stripes_dev call
+    rebuilds every chunk's lost data shares in place -- one mixed-row launch
+    (rs_apply_desc_mix) for the chunks that lost 1-4 data shares, one more
+    per larger count. Self-checked: lost rows wiped, rebuilt, compared with
+    the pristine data. Calls back to back on one stream (each call's host
+    work -- patterns, records, descriptor upload -- overlaps the previous
+    call's kernels), HIP events around `reps` calls. Algorithmic bytes per
+    call: sum over chunks with e > 0 lost data shares of (k + e) * B."""
+    k, n, B, N = w.k, w.n, w.B, w.N
+    sp = stream.cuda_stream
+    sets = download_sets(k, n, N, SEED_BASE + 4242)
+    lost = [[j for j in range(k) if j not in sorted(x)[:k]] for x in sets]
+    ids, cnt = _lib.encode_stripe_shares(sets)
+    w.encode()
+    ref = w.data.clone()
+    view = w.data.view(N, k, B)
+    with torch.cuda.stream(stream):
+        for si, ls in enumerate(lost):
+            for e in ls:
+                view[si, e].zero_()
+    ctx.decode_stripes_dev_raw(k, n, B, N, ids, cnt, w.dptr, w.pptr, w.dptr, stream=sp)
+    stream.synchronize()
+    if not torch.equal(w.data, ref):
+        raise SystemExit("download decode round trip mismatch")
+    del ref
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        ctx.decode_stripes_dev_raw(k, n, B, N, ids, cnt, w.dptr, w.pptr, w.dptr, stream=sp)
+    e0.record(stream)
+    for _ in range(reps):
+        ctx.decode_stripes_dev_raw(k, n, B, N, ids, cnt, w.dptr, w.pptr, w.dptr, stream=sp)
+    e1.record(stream)
+    stream.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    alg = sum((k + len(x)) * B for x in lost if x)
+    hist = {}
+    for x in lost:
+        hist[len(x)] = hist.get(len(x), 0) + 1
+    achieved = alg / (ms * 1e-3) / 1e9
+    res = {"value": round(N * w.chunk / GIB / (ms * 1e-3), 2), "unit": "GiB/s",
+           "what": "GiB/s of chunks reconstructed (device-resident), per-chunk survivor sets "
+                   "from simulated download arrivals, one storb_rs_decode_stripes_dev per batch",
+           "ms_per_call": round(ms, 4), "calls": reps,
+           "kernel": f"rs_apply_desc_mix<{min(k, 32)}>",
+           "lost_data_shares_histogram": dict(sorted(hist.items())),
+           "distinct_patterns": len({tuple(sorted(x)[:k]) for x in sets}),
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes_per_call": alg}}
+    if not a.no_traffic:
+        t = pmc_download_traffic(a, w)
+        res["roofline"]["traffic"] = t.get("traffic")
+        res["roofline"]["traffic_source"] = t.get("traffic_source")
+        if t.get("traffic"):
+            res["roofline"]["traffic_vs_algorithmic"] = round(t["traffic"] / alg, 5)
+    return res
 
 
 def repair_rate(ctx, w, stream, reps=5):
@@ -610,26 +745,22 @@ def leg_kernel_match(a, w, leg):
     return f"rs_apply_{'lds' if a.kernel == 'lds' else 'perm'}<{kb}, {r if r <= 8 else 16},"
 
 
-def pmc_traffic(a, w):
-    """HBM bytes per launch measured in THIS run (roofline.traffic): two short
-    child runs of the same workload under rocprofv3, one per counter
-    (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), each under a hard
-    time limit. gfx950 correction (MI355X_MICROARCH.md, HBM): read bytes =
-    2 x FETCH_SIZE KiB for 16-B-per-lane streaming loads; WRITE_SIZE is exact
-    for 16-B-per-lane stores. Per leg: median over that kernel's launches."""
+def _pmc_passes(a, erase_pattern, seq=False):
+    """Two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child
+    run of this workload: ({(kernel name, counter): [values in launch
+    order]}, error or None)."""
     import csv
     import glob
     import shutil
-    import statistics
     import subprocess
     import tempfile
 
     prof = shutil.which("rocprofv3")
     if not prof:
-        return {"traffic": None, "traffic_source": "rocprofv3 not found"}
+        return None, "rocprofv3 not found"
     child = [sys.executable, os.path.abspath(__file__), "--config", str(a.config),
              "--steps", "3", "--warmup", "1", "--minimal", "--no-check", "--kernel", a.kernel,
-             "--objects", str(a.objects), "--erase-pattern", a.erase_pattern,
+             "--objects", str(a.objects), "--erase-pattern", erase_pattern,
              "--fail", str(a.fail)]
     if a.chunks:
         child += ["--chunks", str(a.chunks)]
@@ -637,7 +768,6 @@ def pmc_traffic(a, w):
         child += ["--erase", str(a.erase)]
     env = dict(os.environ, TMPDIR="/tmp")
     vals = {}
-    t0 = time.perf_counter()
     for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="storb_pmc_", dir="/tmp")
         try:
@@ -647,19 +777,74 @@ def pmc_traffic(a, w):
                                stderr=subprocess.PIPE, text=True)
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if r.returncode != 0 or not files:
-                return {"traffic": None,
-                        "traffic_source": f"rocprofv3 --pmc {cnt} failed (rc {r.returncode}): "
-                                          f"{r.stderr.strip()[-300:]}"}
+                return None, (f"rocprofv3 --pmc {cnt} failed (rc {r.returncode}): "
+                              f"{r.stderr.strip()[-300:]}")
             for row in csv.DictReader(open(files[0])):
                 if row["Counter_Name"] == cnt:
                     vals.setdefault((row["Kernel_Name"], cnt), []).append(
                         float(row["Counter_Value"]))
         finally:
             shutil.rmtree(d, ignore_errors=True)
+    return vals, None
+
+
+def pmc_download_traffic(a, w):
+    """HBM bytes of one download decode (--erase-pattern download's decode
+    leg: the mixed-row descriptor launch plus any per-count launch), live,
+    over a child run with download patterns: summed over the rs_apply_desc*
+    launches of the run, divided by its number of decode calls (one
+    rs_apply_desc_mix launch each). The descriptor copy kernel reads
+    page-locked host memory and is not counted."""
+    import statistics
+    vals, err = _pmc_passes(a, "download")
+    if err:
+        return {"traffic": None, "traffic_source": err}
+    f = sum(v for (kn, c), xs in vals.items() if c == "FETCH_SIZE" and "rs_apply_desc" in kn
+            for v in xs)
+    wr = sum(v for (kn, c), xs in vals.items() if c == "WRITE_SIZE" and "rs_apply_desc" in kn
+             for v in xs)
+    calls = [len(xs) for (kn, c), xs in vals.items() if c == "FETCH_SIZE" and "rs_apply_desc_mix" in kn]
+    if not calls or not calls[0]:
+        return {"traffic": None, "traffic_source": "no rs_apply_desc_mix launches in the PMC passes"}
+    b = (2 * f * 1024 + wr * 1024) / calls[0]
+    per = [2 * x * 1024 for (kn, c), xs in vals.items() if c == "FETCH_SIZE"
+           and "rs_apply_desc_mix" in kn for x in xs]
+    return {"traffic": b, "decode_calls": calls[0],
+            "mix_launch_read_bytes_median": statistics.median(per) if per else None,
+            "traffic_source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 3-step "
+                              "child run with --erase-pattern download; read = 2 x FETCH_SIZE"}
+
+
+def pmc_traffic(a, w):
+    """HBM bytes per launch measured in THIS run (roofline.traffic): two short
+    child runs of the same workload under rocprofv3, one per counter
+    (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), each under a hard
+    time limit. gfx950 correction (MI355X_MICROARCH.md, HBM): read bytes =
+    2 x FETCH_SIZE KiB for 16-B-per-lane streaming loads; WRITE_SIZE is exact
+    for 16-B-per-lane stores. Per leg: median over that kernel's launches; a
+    download-pattern decode leg (several launches): the sum over its
+    rs_apply_desc* launches per call."""
+    import statistics
+
+    t0 = time.perf_counter()
+    vals, err = _pmc_passes(a, a.erase_pattern)
+    if err:
+        return {"traffic": None, "traffic_source": err}
     by_leg = {}
     for leg in w.legs:
         if leg == "decode" and w.sets is not None:
-            by_leg[leg] = None  # several launches of different sizes per leg: not per-launch
+            calls = [len(xs) for (kn, c), xs in vals.items()
+                     if c == "FETCH_SIZE" and "rs_apply_desc_mix" in kn]
+            f = sum(v for (kn, c), xs in vals.items() if c == "FETCH_SIZE"
+                    and "rs_apply_desc" in kn for v in xs)
+            wr = sum(v for (kn, c), xs in vals.items() if c == "WRITE_SIZE"
+                     and "rs_apply_desc" in kn for v in xs)
+            if not calls or not calls[0]:
+                by_leg[leg] = None
+                continue
+            b = (2 * f + wr) * 1024 / calls[0]
+            by_leg[leg] = {"kernel": "rs_apply_desc*", "calls": calls[0], "bytes": b,
+                           "vs_algorithmic": round(b / w.alg_bytes(leg), 5)}
             continue
         sub = leg_kernel_match(a, w, leg)
         f = [v for (kn, c), xs in vals.items() if c == "FETCH_SIZE" and sub in kn for v in xs]
@@ -881,7 +1066,7 @@ def line_extras(rank, world, minimal, config):
         return ex
     ex |= {"traffic", "copy_ceiling"}
     if config in (2, 5, 6):
-        ex |= {"cpu_threads", "host_path", "shim_path", "hashing", "repair"}
+        ex |= {"cpu_threads", "host_path", "shim_path", "hashing", "repair", "download"}
     if config == 3:
         ex.add("assembly")
     if config == 4:
@@ -1133,13 +1318,16 @@ def main():
         out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
                                                nchunks=max(8, (256 << 20) // w.chunk),
                                                erased=[e for e in w.fixed_erased if e < w.k],
-                                               sets=w.sets)
+                                               sets=w.sets or download_sets(
+                                                   w.k, w.n, 64, SEED_BASE + 4343))
     if "shim_path" in ex:
         out["shim_path"] = shim_path_rate(ctx)
     if "hashing" in ex:
         out["shard_hashing"] = shard_hash_rate(ctx, w, stream)
     if "repair" in ex:
         out["repair"] = repair_rate(ctx, w, stream)
+    if "download" in ex and w.sets is None and "decode" in w.legs:
+        out["download_decode"] = download_leg(ctx, w, stream, a)
     if "assembly" in ex:
         out["assembly"] = config3_assembly(ctx, w, stream)
     if "storb_faithful" in ex:

@@ -46,6 +46,7 @@ extern "C" {
 #define STORB_RS_ENODEV 5     /* no usable gfx950 device */
 #define STORB_RS_EAGAIN 6     /* storb_rs_op_test: the op's device work is still running */
 #define STORB_RS_EBUSY 7      /* 64 unfinished async ops on the context already */
+#define STORB_RS_ECLOSED 8    /* the async op's context was destroyed before storb_rs_op_finish */
 
 #define STORB_RS_MAX_SHARES 256 /* zfec: n <= 256 */
 
@@ -59,10 +60,29 @@ int storb_rs_device_count(void);
 /* device_ordinal >= 0 pins the context to that GPU; -1 picks devices
  * round-robin across contexts (objects partition across GPUs). */
 int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out);
+/* Waits for everything the context queued, returns its device memory
+ * (stream-ordered pool memory included) and frees it. Async ops started on
+ * it and not yet finished are waited for and detached: storb_rs_op_test and
+ * storb_rs_op_finish on them return STORB_RS_ECLOSED without touching the
+ * destroyed context (finish still frees the op; outputs staged for finish
+ * are not written). */
 void storb_rs_ctx_destroy(storb_rs_ctx *ctx);
 int storb_rs_ctx_device(const storb_rs_ctx *ctx);
 /* Detail of the last failure on this context ("" if none). */
 const char *storb_rs_last_error(const storb_rs_ctx *ctx);
+/* Counters of a context (diagnostics, tests). */
+typedef struct {
+  uint64_t streamed_calls;   /* single calls completed on the streamed path */
+  uint64_t stream_fallbacks; /* streamed attempts a workgroup gave up on (redone sliced) */
+  uint64_t sliced_calls;     /* single calls on the column-sliced path */
+  uint64_t live_ops;         /* async ops started and not finished */
+  uint64_t tables;           /* cached coefficient tables */
+} storb_rs_ctx_stats_t;
+int storb_rs_ctx_stats(const storb_rs_ctx *ctx, storb_rs_ctx_stats_t *out);
+/* Bytes in use / reserved in the device's default stream-ordered memory pool
+ * (where the contexts' coefficient tables live, hipMallocAsync): a destroyed
+ * context leaves "used" where it found it. */
+int storb_rs_device_pool_stats(int device, uint64_t *used, uint64_t *reserved);
 
 /* ---- code parameters (host only, no GPU needed) ----------------------- */
 /* zfec-rs Fec::new validation: STORB_RS_OK or STORB_RS_EINVAL. */
@@ -87,6 +107,15 @@ int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                     const uint8_t *data, size_t len,
                     uint8_t *const *parity_out, size_t *block_out,
                     size_t *padlen_out);
+/* zfec-rs Fec::encode's full result (piece.rs:329: all m shares in index
+ * order): shares_out[0..k) receive the data shares (B bytes each, the last
+ * zero-padded), shares_out[k..n) the parity. The data shares are copied by
+ * the host copy pool while the kernel computes the parity, so a shim that
+ * must return every share pays no serial copy of its own. */
+int storb_rs_encode_shares(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                           const uint8_t *data, size_t len,
+                           uint8_t *const *shares_out, size_t *block_out,
+                           size_t *padlen_out);
 /* Decode one chunk from nshares >= k shares (any order). Selection follows
  * decode_chunk (piece.rs:368-381): sort by index, keep the first k. Writes
  * k*block - padlen bytes to out. */
@@ -141,6 +170,8 @@ int storb_rs_decode_chunks(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
  * Memory from storb_rs_host_alloc, or a caller range made page-locked with
  * storb_rs_host_register, qualifies; the check is by address range. */
 int storb_rs_host_alloc(size_t len, void **out);
+/* storb_rs_host_free / _unregister wait for every device of the process
+ * before the range is unmapped (a kernel may still be reading it). */
 int storb_rs_host_free(void *p); /* only pointers from storb_rs_host_alloc */
 int storb_rs_host_register(void *p, size_t len);
 int storb_rs_host_unregister(void *p);
@@ -292,7 +323,8 @@ int storb_rs_jit_prepare_decode(uint32_t k, uint32_t n, const uint32_t *share_id
  * device work (k = 1, nothing missing). storb_rs_op_test polls (STORB_RS_OK
  * when done, STORB_RS_EAGAIN while running); storb_rs_op_finish waits if
  * needed, writes the outputs, frees the op and returns its result. Finish
- * every op exactly once, before destroying its context. Ops of a context run
+ * every op exactly once, before destroying its context (an op outliving its
+ * context finishes with STORB_RS_ECLOSED, see storb_rs_ctx_destroy). Ops of a context run
  * concurrently (one stream and staging slot each, reused after finish); with
  * 64 unfinished the call returns STORB_RS_EBUSY. On any error no op is
  * returned. */

@@ -15,6 +15,9 @@ use std::ffi::CStr;
 use std::fmt;
 use std::os::raw::{c_char, c_int};
 
+/// Batched, hashed, async and page-locked calls beyond the zfec-rs API.
+pub mod mi355x;
+
 #[repr(C)]
 pub struct StorbRsCtx {
     _private: [u8; 0],
@@ -27,13 +30,13 @@ extern "C" {
     fn storb_rs_last_error(ctx: *const StorbRsCtx) -> *const c_char;
     fn storb_rs_check_params(k: u32, n: u32) -> c_int;
     fn storb_rs_block_size(k: u32, len: usize) -> usize;
-    fn storb_rs_encode(
+    fn storb_rs_encode_shares(
         ctx: *mut StorbRsCtx,
         k: u32,
         n: u32,
         data: *const u8,
         len: usize,
-        parity_out: *const *mut u8,
+        shares_out: *const *mut u8,
         block_out: *mut usize,
         padlen_out: *mut usize,
     ) -> c_int;
@@ -138,27 +141,31 @@ impl Fec {
         Ok(Fec { k, m })
     }
 
-    /// All `m` shares in index order and the zero-padding length.
+    /// All `m` shares in index order and the zero-padding length. One call
+    /// writes every share: the library copies the k data shares (the last
+    /// one zero-padded) on its host pool while the kernel computes parity,
+    /// so the shim neither zero-fills nor copies anything itself.
     pub fn encode(&self, data: &[u8]) -> Result<(Vec<Chunk>, usize), Error> {
         let (k, m) = (self.k, self.m);
         let b = unsafe { storb_rs_block_size(k as u32, data.len()) };
-        let mut chunks: Vec<Chunk> = (0..m).map(|i| Chunk::new(vec![0u8; b], i)).collect();
-        for (j, c) in chunks.iter_mut().take(k).enumerate() {
-            let off = j * b;
-            if off < data.len() {
-                let end = std::cmp::min(off + b, data.len());
-                c.data[..end - off].copy_from_slice(&data[off..end]);
-            }
-        }
-        let parity: Vec<*mut u8> = chunks[k..].iter_mut().map(|c| c.data.as_mut_ptr()).collect();
+        let mut bufs: Vec<Vec<u8>> = (0..m).map(|_| Vec::with_capacity(b.max(1))).collect();
+        let ptrs: Vec<*mut u8> = bufs.iter_mut().map(|v| v.as_mut_ptr()).collect();
         let (mut block, mut pad) = (0usize, 0usize);
         with_ctx(|ctx| {
             let rc = unsafe {
-                storb_rs_encode(ctx, k as u32, m as u32, data.as_ptr(), data.len(),
-                                parity.as_ptr(), &mut block, &mut pad)
+                storb_rs_encode_shares(ctx, k as u32, m as u32, data.as_ptr(), data.len(),
+                                       ptrs.as_ptr(), &mut block, &mut pad)
             };
             if rc != 0 { Err(error(rc, ctx)) } else { Ok(()) }
         })?;
+        let chunks = bufs
+            .into_iter()
+            .enumerate()
+            .map(|(i, mut v)| {
+                unsafe { v.set_len(b) } // all b bytes written by storb_rs_encode_shares
+                Chunk::new(v, i)
+            })
+            .collect();
         Ok((chunks, pad))
     }
 
@@ -174,7 +181,8 @@ impl Fec {
         }
         let ptrs: Vec<*const u8> = encoded_data.iter().map(|c| c.data.as_ptr()).collect();
         let idx: Vec<u32> = encoded_data.iter().map(|c| c.index as u32).collect();
-        let mut out = vec![0u8; k * b - padding];
+        let outlen = k * b - padding;
+        let mut out: Vec<u8> = Vec::with_capacity(outlen);
         with_ctx(|ctx| {
             let rc = unsafe {
                 storb_rs_decode(ctx, k as u32, self.m as u32, ptrs.as_ptr(), idx.as_ptr(),
@@ -182,6 +190,7 @@ impl Fec {
             };
             if rc != 0 { Err(error(rc, ctx)) } else { Ok(()) }
         })?;
+        unsafe { out.set_len(outlen) } // every byte written by storb_rs_decode
         Ok(out)
     }
 }

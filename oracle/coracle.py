@@ -50,6 +50,9 @@ def lib():
         L.zo_splitmix_fill.argtypes = [C.c_uint64, C.c_void_p, C.c_size_t]
         L.zo_encode_many.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_size_t, C.c_uint,
                                      C.c_void_p, C.c_int]
+        L.zo_bench_roundtrip.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_size_t, C.c_uint,
+                                         C.POINTER(C.c_uint), C.c_uint, C.c_int, C.c_int,
+                                         C.c_int, C.c_double, C.c_void_p]
         L.zo_roundtrip_many.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_size_t, C.c_uint,
                                         C.POINTER(C.c_uint), C.c_uint, C.c_int]
         _lib = L
@@ -127,3 +130,29 @@ def roundtrip_many(k: int, n: int, data: np.ndarray, chunk_len: int, nchunks: in
     er = (C.c_uint * max(1, len(erased)))(*erased)
     return int(lib().zo_roundtrip_many(k, n, _ptr(data), chunk_len, nchunks, er, len(erased),
                                        threads))
+
+
+class BenchStats(C.Structure):
+    """zo_bench_t (oracle/zfec_oracle.h)."""
+    _fields_ = [("wall_s", C.c_double), ("user_s", C.c_double), ("sys_s", C.c_double),
+                ("minflt", C.c_long), ("majflt", C.c_long), ("nvcsw", C.c_long),
+                ("nivcsw", C.c_long), ("calls", C.c_ulonglong), ("cpu_start", C.c_int),
+                ("cpu_end", C.c_int), ("bad", C.c_int)]
+
+
+def bench_roundtrip(k: int, n: int, chunks: np.ndarray, chunk_len: int, nsample: int,
+                    survivor_sets, do_encode: bool, do_decode: bool, fresh: bool,
+                    seconds: float) -> dict:
+    """The CPU baseline loop in C on the calling thread (oracle/cpu_bench.c)
+    with that thread's getrusage accounting. fresh: per-call buffers as
+    zfec-rs allocates them; else every buffer allocated once."""
+    sets = [list(s)[:k] for s in survivor_sets]
+    flat = (C.c_uint * (k * len(sets)))(*[i for s in sets for i in s])
+    st = BenchStats()
+    buf = np.ascontiguousarray(chunks, dtype=np.uint8)
+    rc = lib().zo_bench_roundtrip(k, n, buf.ctypes.data, chunk_len, nsample, flat, len(sets),
+                                  int(do_encode), int(do_decode), int(fresh), float(seconds),
+                                  C.addressof(st))
+    if rc != 0 or st.bad:
+        raise ValueError(f"zo_bench_roundtrip rc={rc} bad={st.bad}")
+    return {f: getattr(st, f) for f, _ in BenchStats._fields_}

@@ -202,18 +202,22 @@ int zo_fec_new(unsigned k, unsigned n, uint8_t *enc) {
 /* ------------------------------------------------------------- encode */
 #define ZO_STRIDE 8192 /* fec.c STRIDE blocking of the addmul loop */
 
-static int encode_impl(unsigned k, unsigned n, const uint8_t *data,
-                       size_t len, uint8_t *const *out_rows, int parity_only,
-                       size_t *block_out, size_t *padlen_out) {
+/* scratch (k*B bytes) / enc (n*k): caller-provided buffers for the
+ * allocation-free CPU baseline (cpu_bench.c); NULL = allocate per call, as
+ * zfec-rs does (a Fec per chunk, piece.rs:328; Vecs per share). */
+int zo_encode_impl(unsigned k, unsigned n, const uint8_t *data, size_t len,
+                   uint8_t *const *out_rows, int parity_only, size_t *block_out,
+                   size_t *padlen_out, uint8_t *scratch, uint8_t *enc_in) {
   zo_init();
   if (k < 1 || n < 1 || n > 256 || k > n || len == 0) return -1;
-  uint8_t *enc = malloc((size_t)n * k);
+  uint8_t *enc = enc_in ? enc_in : malloc((size_t)n * k);
   zo_fec_new(k, n, enc);
   size_t B = (len + k - 1) / k; /* piece.rs:331-332 div_ceil(len, k) */
   size_t pad = B * k - len;
   /* zero-padded copies of the k data shards (zfec-rs splits into Vecs). */
-  uint8_t *shards = calloc((size_t)k * B, 1);
+  uint8_t *shards = scratch ? scratch : calloc((size_t)k * B, 1);
   memcpy(shards, data, len);
+  if (scratch && pad) memset(shards + len, 0, pad);
   unsigned first = parity_only ? k : 0;
   for (unsigned i = first; i < n; i++) {
     uint8_t *dst = out_rows[i - first];
@@ -231,8 +235,8 @@ static int encode_impl(unsigned k, unsigned n, const uint8_t *data,
         addmul(dst, shards + (size_t)j * B + off, enc[(size_t)i * k + j], sz);
     }
   }
-  free(shards);
-  free(enc);
+  if (!scratch) free(shards);
+  if (!enc_in) free(enc);
   if (block_out) *block_out = B;
   if (padlen_out) *padlen_out = pad;
   return 0;
@@ -244,7 +248,7 @@ int zo_encode(unsigned k, unsigned n, const uint8_t *data, size_t len,
   size_t B = (len + k - 1) / k;
   uint8_t **rows = malloc(sizeof(uint8_t *) * n);
   for (unsigned i = 0; i < n; i++) rows[i] = shares + (size_t)i * B;
-  int rc = encode_impl(k, n, data, len, rows, 0, block_out, padlen_out);
+  int rc = zo_encode_impl(k, n, data, len, rows, 0, block_out, padlen_out, NULL, NULL);
   free(rows);
   return rc;
 }
@@ -252,13 +256,21 @@ int zo_encode(unsigned k, unsigned n, const uint8_t *data, size_t len,
 int zo_encode_parity(unsigned k, unsigned n, const uint8_t *data, size_t len,
                      uint8_t *const *parity, size_t *block_out,
                      size_t *padlen_out) {
-  return encode_impl(k, n, data, len, parity, 1, block_out, padlen_out);
+  return zo_encode_impl(k, n, data, len, parity, 1, block_out, padlen_out, NULL, NULL);
 }
 
 /* ------------------------------------------------------------- decode */
 int zo_decode(unsigned k, unsigned n, const uint8_t *const *shares,
               const unsigned *idx, unsigned nshares, size_t B, size_t padlen,
               uint8_t *out) {
+  return zo_decode_impl(k, n, shares, idx, nshares, B, padlen, out, NULL);
+}
+
+/* row_scratch (B bytes): the allocation-free baseline's buffer for the
+ * rebuilt row; NULL = allocate per call. */
+int zo_decode_impl(unsigned k, unsigned n, const uint8_t *const *shares,
+                   const unsigned *idx, unsigned nshares, size_t B, size_t padlen,
+                   uint8_t *out, uint8_t *row_scratch) {
   zo_init();
   if (k < 1 || n < 1 || n > 256 || k > n || B == 0 || padlen >= (size_t)k * B + 1)
     return -1;
@@ -318,7 +330,7 @@ int zo_decode(unsigned k, unsigned n, const uint8_t *const *shares,
   int rc = zo_invert_mat(dm, k);
   if (rc == 0) {
     size_t outlen = (size_t)k * B - padlen;
-    uint8_t *row = malloc(B);
+    uint8_t *row = row_scratch ? row_scratch : malloc(B);
     for (unsigned r = 0; r < k; r++) {
       const uint8_t *src = slot[r];
       if (slot_idx[r] >= k) {
@@ -333,7 +345,7 @@ int zo_decode(unsigned k, unsigned n, const uint8_t *const *shares,
         memcpy(out + off, src, cnt);
       }
     }
-    free(row);
+    if (!row_scratch) free(row);
   } else {
     rc = -2;
   }
@@ -411,8 +423,8 @@ static void *many_worker(void *arg) {
   for (unsigned c = j->first; c < j->last; c++) {
     for (unsigned r = 0; r < p; r++)
       rows[r] = j->parity + ((size_t)c * p + r) * B;
-    encode_impl(j->k, j->n, j->data + (size_t)c * j->len, j->len, rows, 1,
-                NULL, NULL);
+    zo_encode_impl(j->k, j->n, j->data + (size_t)c * j->len, j->len, rows, 1,
+                   NULL, NULL, NULL, NULL);
   }
   free(rows);
   return NULL;

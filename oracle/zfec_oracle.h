@@ -63,6 +63,32 @@ int zo_encode_parity(unsigned k, unsigned n, const uint8_t *data, size_t len,
 int zo_decode(unsigned k, unsigned n, const uint8_t *const *shares,
               const unsigned *idx, unsigned nshares, size_t block,
               size_t padlen, uint8_t *out);
+/* The same with caller-provided scratch (NULL = allocate per call, the
+ * reference's behaviour): encode's zero-padded data copy (k*B) and
+ * generator (n*k), decode's rebuilt row (B). */
+int zo_encode_impl(unsigned k, unsigned n, const uint8_t *data, size_t len,
+                   uint8_t *const *out_rows, int parity_only, size_t *block_out,
+                   size_t *padlen_out, uint8_t *scratch, uint8_t *enc);
+int zo_decode_impl(unsigned k, unsigned n, const uint8_t *const *shares,
+                   const unsigned *idx, unsigned nshares, size_t block, size_t padlen,
+                   uint8_t *out, uint8_t *row_scratch);
+
+/* CPU baseline loop (cpu_bench.c), timed and accounted on the calling
+ * thread: encode and/or decode round trips over nsample chunks of len bytes
+ * (chunk i at chunks + i*len), survivor set (i mod nsets) of surv (k each),
+ * until `seconds` of wall time. fresh = 1: every call allocates its outputs
+ * as zfec-rs does (Vec per share, Vec out; the oracle's own per-call
+ * buffers); fresh = 0: all buffers allocated once (arithmetic only). */
+typedef struct {
+  double wall_s, user_s, sys_s;
+  long minflt, majflt, nvcsw, nivcsw;
+  unsigned long long calls;
+  int cpu_start, cpu_end;
+  int bad;
+} zo_bench_t;
+int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len,
+                       unsigned nsample, const unsigned *surv, unsigned nsets, int do_encode,
+                       int do_decode, int fresh, double seconds, zo_bench_t *out);
 
 /* Storb sizing: piece_length (piece.rs:292-303; 0 = default bounds) and
  * get_k_and_m (piece.rs:307-317; m = TOTAL share count). */

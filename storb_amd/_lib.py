@@ -25,6 +25,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libstorb_rs.so")
 
 OK, EINVAL, ENOTENOUGH, EDEVICE, ENOMEM, ENODEV = range(6)
+EAGAIN, EBUSY, ECLOSED = 6, 7, 8
 KERNEL_AUTO, KERNEL_PERM, KERNEL_LDS = 0, 1, 2
 
 
@@ -56,6 +57,12 @@ class JitStats(C.Structure):
                 ("evicted", C.c_uint64), ("loaded", C.c_uint64)]
 
 
+class CtxStats(C.Structure):
+    """storb_rs_ctx_stats_t (include/storb_rs.h)."""
+    _fields_ = [("streamed_calls", C.c_uint64), ("stream_fallbacks", C.c_uint64),
+                ("sliced_calls", C.c_uint64), ("live_ops", C.c_uint64), ("tables", C.c_uint64)]
+
+
 NOTIFY_FN = C.CFUNCTYPE(None, vp)  # storb_rs_notify_fn
 
 
@@ -80,6 +87,10 @@ def _declare(L):
     L.storb_get_k_and_m.restype = None
     L.storb_rs_encode.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.POINTER(vp),
                                   C.POINTER(sz), C.POINTER(sz)]
+    L.storb_rs_encode_shares.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.POINTER(vp),
+                                         C.POINTER(sz), C.POINTER(sz)]
+    L.storb_rs_ctx_stats.argtypes = [vp, C.POINTER(CtxStats)]
+    L.storb_rs_device_pool_stats.argtypes = [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.storb_rs_decode.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(vp),
                                   C.POINTER(C.c_uint32), C.c_uint32, sz, sz, vp]
     L.storb_rs_encode_chunks.argtypes = [vp, C.c_uint32, C.c_uint32, vp, sz, C.c_uint32, vp]
@@ -156,6 +167,15 @@ def version() -> str:
 
 def device_count() -> int:
     return int(lib().storb_rs_device_count())
+
+
+def device_pool_stats(device: int = 0) -> tuple[int, int]:
+    """(used, reserved) bytes of the device's default stream-ordered pool."""
+    u, r = C.c_uint64(), C.c_uint64()
+    rc = lib().storb_rs_device_pool_stats(device, C.byref(u), C.byref(r))
+    if rc != OK:
+        raise StorbRsError(rc, "storb_rs_device_pool_stats")
+    return int(u.value), int(r.value)
 
 
 def check_params(k: int, n: int) -> bool:
@@ -265,6 +285,10 @@ class Context:
         if rc != OK:
             raise StorbRsError(rc, "storb_rs_ctx_create")
         self._h = h
+        # Async ops started here and not finished: close() detaches them
+        # (storb_rs_ctx_destroy waits for their device work; finish() then
+        # raises ECLOSED instead of touching the destroyed context).
+        self._ops = weakref.WeakSet()
         # hipStream_t used when a call passes stream=None. None here means
         # NULL at the ABI: the HIP null stream, which orders with torch's
         # default stream and which sync() waits for. Tests point it at
@@ -283,9 +307,23 @@ class Context:
         return int(lib().storb_rs_ctx_device(self._h))
 
     def close(self):
+        """Destroy the context. Unfinished AsyncOps of it are waited for and
+        detached: their finish() / test() raise StorbRsError(ECLOSED)."""
         if getattr(self, "_h", None):
             lib().storb_rs_ctx_destroy(self._h)
             self._h = None
+            for op in list(getattr(self, "_ops", ())):
+                op._ctx_closed = True
+
+    @property
+    def closed(self) -> bool:
+        return not getattr(self, "_h", None)
+
+    def stats(self) -> dict:
+        """storb_rs_ctx_stats: single-call path counters, live async ops, tables."""
+        st = CtxStats()
+        self._check(lib().storb_rs_ctx_stats(self._h, C.byref(st)), "storb_rs_ctx_stats")
+        return {f: getattr(st, f) for f, _ in CtxStats._fields_}
 
     def __del__(self):
         try:
@@ -310,6 +348,22 @@ class Context:
                                    buf.size, ptrs, C.byref(b), C.byref(pad))
         self._check(rc, "storb_rs_encode")
         return [o[: b.value].tobytes() for o in outs], int(b.value), int(pad.value)
+
+    def encode_shares(self, k: int, n: int, data, shares: Optional[Sequence[np.ndarray]] = None):
+        """storb_rs_encode_shares: all n shares (data shares zero-padded, then
+        parity), zfec-rs Fec::encode's result. shares: optional caller-owned
+        arrays (n of >= B bytes). Returns (shares, B, padlen)."""
+        buf = _as_u8(data)
+        B = block_size(k, buf.size) if k else 0
+        outs = list(shares) if shares is not None else \
+            [np.empty(max(B, 1), dtype=np.uint8) for _ in range(max(n, 0))]
+        assert len(outs) == n
+        ptrs = (vp * max(n, 1))(*[o.ctypes.data for o in outs])
+        b, pad = sz(), sz()
+        rc = lib().storb_rs_encode_shares(self._h, k, n, buf.ctypes.data if buf.size else None,
+                                          buf.size, ptrs, C.byref(b), C.byref(pad))
+        self._check(rc, "storb_rs_encode_shares")
+        return [o[: b.value] for o in outs], int(b.value), int(pad.value)
 
     def decode(self, k: int, n: int, shares: Sequence, idx: Sequence[int], block: int,
                padlen: int) -> bytes:
@@ -653,6 +707,8 @@ class AsyncOp:
 
     def __init__(self, ctx: Context, notify=None):
         self._ctx = ctx  # keeps the context alive until finish
+        self._ctx_closed = False  # set by ctx.close() while this op is unfinished
+        ctx._ops.add(self)
         self._st = _OpState()
         self._h = self._st.h
         self._keep = None

@@ -16,9 +16,11 @@
 
 #include <cstdint>
 #include <functional>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -94,13 +96,11 @@ struct Tables {
   std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // last use per stream
   uint64_t tick = 0;              // LRU clock
   ~Tables() {
-    // dev is pool memory (hipMallocAsync): eviction and context teardown
-    // return it with hipFreeAsync (storb_rs.cpp release_table); only a table
-    // whose release failed gets here with it, freed the same way.
-    if (dev) {
-      (void)hipFreeAsync(dev, nullptr);
-      (void)hipStreamSynchronize(nullptr);
-    }
+    // dev is pool memory (hipMallocAsync). Eviction and context teardown give
+    // it back stream-ordered (storb_rs.cpp release_table, after the upload
+    // and the last use on every stream); teardown frees a table whose release
+    // failed itself, after a device synchronisation. Nothing is freed here:
+    // a destructor has no stream the free could be ordered on.
     if (uploaded) (void)hipEventDestroy(uploaded);
     for (auto &u : uses) (void)hipEventDestroy(u.second);
   }
@@ -145,6 +145,8 @@ struct DeviceGuard {
 
 }  // namespace detail
 }  // namespace storb_rs
+
+struct storb_rs_op;
 
 struct storb_rs_ctx {
   int device = 0;
@@ -194,9 +196,26 @@ struct storb_rs_ctx {
   hipEvent_t desc_copied = nullptr;
   unsigned desc_next = 0;
   // Slots of the asynchronous host calls (host_async.cpp); async_mu guards
-  // the busy flags, which finish() clears without holding mu.
+  // the busy flags, which finish() clears without holding mu, and the set of
+  // ops started and not yet finished, which storb_rs_ctx_destroy invalidates
+  // (an op finished after its context is gone must not touch it).
   std::mutex async_mu;
   std::vector<std::unique_ptr<storb_rs::detail::AsyncSlot>> async_slots;
+  std::set<storb_rs_op *> live_ops;
+  // Single-call path counters (storb_rs_ctx_stats).
+  std::atomic<uint64_t> n_streamed{0}, n_stream_fallbacks{0}, n_sliced{0};
+  // Streamed single calls: how long a workgroup waits for its slice's ready
+  // word (s_memrealtime ticks, 100 MHz) and how long the host waits for a
+  // done word before it drains the stream and looks again (ms). Test knob
+  // (read once, at context creation): STORB_RS_TEST_STREAM_STALL=
+  // "<ticks>,<host ms>,<slice>,<us>,<calls>" shortens both and, in the first
+  // <calls> streamed calls, makes the host sleep <us> before publishing slice
+  // <slice>, so a test can force the give-up path (tests/test_gpu_runtime.py).
+  uint64_t stream_timeout_ticks = 100000000ull;
+  int stream_host_wait_ms = 500;
+  uint32_t test_stall_slice = UINT32_MAX;
+  uint32_t test_stall_us = 0;
+  uint32_t test_stall_calls = 0;
 };
 
 namespace storb_rs {
@@ -290,12 +309,18 @@ bool desc_ok(const storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block);
 // reading / writing the caller's page-locked buffers).
 void drain_streams(storb_rs_ctx *ctx);
 hipStream_t pick_stream(storb_rs_ctx *ctx, void *s);
+// storb_rs_ctx_destroy: every op started on ctx and not finished is
+// detached from it (host_async.cpp).
+void invalidate_ops(storb_rs_ctx *ctx);
 // Device address of page-locked host memory.
 hipError_t host_dev_ptr(uint8_t *host, uint8_t **dev);
 // Single-call pipeline over column slices of one stripe (host_calls.cpp).
+// `during` (optional) runs on the calling thread after the last slice is
+// launched, overlapping its kernel.
 int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)> &pack,
            const std::function<int(size_t, size_t)> &launch,
-           const std::function<void(size_t, size_t)> &unpack);
+           const std::function<void(size_t, size_t)> &unpack,
+           const std::function<void()> *during = nullptr);
 
 }  // namespace detail
 }  // namespace storb_rs

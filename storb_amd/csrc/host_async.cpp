@@ -46,6 +46,9 @@ struct storb_rs_op {
   storb_rs_ctx *ctx = nullptr;
   AsyncSlot *slot = nullptr;  // null: completed at start (no device work)
   int rc = STORB_RS_OK;
+  // The context was destroyed before finish (storb_rs_ctx_destroy drained
+  // the op's stream and detached it): ctx and slot are gone, rc = ECLOSED.
+  bool closed = false;
   storb_rs_notify_fn notify = nullptr;
   void *user = nullptr;
   // Copies finish() makes from the slot's page-locked output: (dst, offset
@@ -101,11 +104,12 @@ int acquire_slot(storb_rs_ctx *ctx, AsyncSlot **out) {
 // finished, so idle slots never pin more than 64 x 2 x kSlotKeep bytes.
 constexpr size_t kSlotKeep = 32u << 20;
 
-void release_slot(storb_rs_ctx *ctx, AsyncSlot *s) {
+void release_slot(storb_rs_ctx *ctx, AsyncSlot *s, storb_rs_op *op = nullptr) {
   if (s->in.cap > kSlotKeep) s->in.release();
   if (s->out.cap > kSlotKeep) s->out.release();
   std::lock_guard<std::mutex> lk(ctx->async_mu);
   s->busy = false;
+  if (op) ctx->live_ops.erase(op);
 }
 
 // Queue the notification, then record completion on the slot's stream: an
@@ -274,11 +278,33 @@ int finish_start(storb_rs_ctx *ctx, storb_rs_op *op, int rc, storb_rs_op **out) 
     return rc;
   }
   if (!op->slot && op->notify) op->notify(op->user);
+  if (op->slot) {
+    std::lock_guard<std::mutex> lk(ctx->async_mu);
+    ctx->live_ops.insert(op);
+  }
   *out = op;
   return STORB_RS_OK;
 }
 
 }  // namespace
+
+namespace storb_rs {
+namespace detail {
+
+void invalidate_ops(storb_rs_ctx *ctx) {
+  std::lock_guard<std::mutex> lk(ctx->async_mu);
+  for (storb_rs_op *op : ctx->live_ops) {
+    op->closed = true;
+    op->rc = STORB_RS_ECLOSED;
+    op->ctx = nullptr;
+    op->slot = nullptr;
+    op->copies.clear();
+  }
+  ctx->live_ops.clear();
+}
+
+}  // namespace detail
+}  // namespace storb_rs
 
 extern "C" {
 
@@ -320,6 +346,7 @@ int storb_rs_decode_async(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
 
 int storb_rs_op_test(const storb_rs_op *op) {
   if (!op) return STORB_RS_EINVAL;
+  if (op->closed) return STORB_RS_ECLOSED;
   if (!op->slot) return STORB_RS_OK;
   const hipError_t q = hipEventQuery(op->slot->done);
   if (q == hipSuccess) return STORB_RS_OK;
@@ -330,6 +357,10 @@ int storb_rs_op_test(const storb_rs_op *op) {
 int storb_rs_op_finish(storb_rs_op *op) {
   if (!op) return STORB_RS_EINVAL;
   int rc = op->rc;
+  if (op->closed) {  // its context is gone: nothing to wait for or write
+    delete op;
+    return rc;
+  }
   if (op->slot) {
     storb_rs_ctx *ctx = op->ctx;
     DeviceGuard g(ctx->device);
@@ -352,7 +383,7 @@ int storb_rs_op_finish(storb_rs_op *op) {
       else
         for (auto &c : op->copies) std::memcpy(c.dst, src + c.off, c.len);
     }
-    release_slot(ctx, op->slot);
+    release_slot(ctx, op->slot, op);
   }
   delete op;
   return rc;

@@ -10,9 +10,11 @@
 #include <chrono>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
+#include "seq.hpp"
 
 using namespace storb_rs;
 using namespace storb_rs::detail;
@@ -74,7 +76,7 @@ static int slice_signal(storb_rs_ctx *ctx, hipStream_t s, int t, uint32_t *seq) 
     std::memset(ctx->flag_pin.p, 0, kMaxSlices * 64);
     HIP_TRY(ctx, host_dev_ptr(ctx->flag_pin.p, &ctx->flag_dev));
   }
-  *seq = ++ctx->flag_seq;
+  *seq = next_seq(ctx->flag_seq);
   HIP_TRY(ctx, hipStreamWriteValue32(s, ctx->flag_dev + t * 64, *seq, 0));
   return STORB_RS_OK;
 }
@@ -107,7 +109,8 @@ static int slice_wait(storb_rs_ctx *ctx, hipStream_t, int t, uint32_t) {
 
 int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)> &pack,
            const std::function<int(size_t, size_t)> &launch,
-           const std::function<void(size_t, size_t)> &unpack) {
+           const std::function<void(size_t, size_t)> &unpack, const std::function<void()> *during) {
+  ctx->n_sliced++;
   int q = static_cast<int>(std::min<size_t>(kMaxSlices, S / (128u << 10)));
   if (q < 2) q = 1;
   const size_t slice = round_up((S + q - 1) / q, kAlign);
@@ -135,6 +138,7 @@ int sliced(storb_rs_ctx *ctx, size_t S, const std::function<void(size_t, size_t)
       unpack(off, cnt);
     }
   }
+  if (during) (*during)();  // host work that overlaps the last slice's kernel
   size_t off, cnt;
   range(q - 1, off, cnt);
   TMARK("wait");
@@ -160,7 +164,8 @@ constexpr int kNotStreamed = -1;
 int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
              const uint8_t *const *in, uint8_t *const *out, size_t S,
              const std::function<void(size_t, size_t)> &pack,
-             const std::function<void(size_t, size_t)> &unpack, uint32_t enc_n = 0) {
+             const std::function<void(size_t, size_t)> &unpack, uint32_t enc_n = 0,
+             const std::function<void()> *during = nullptr) {
   if (ctx->variant != STORB_RS_KERNEL_AUTO || k == 0 || rows == 0 || S % kAlign)
     return kNotStreamed;
   // Encode of (16, 24) / (32, 48): the bit-sliced encoder's streamed form;
@@ -212,10 +217,10 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
   st.ready = words;
   st.done = words + kMaxStreamSlices * 16;
   st.cnt = reinterpret_cast<uint32_t *>(ctx->scnt.p);
-  st.seq = ++ctx->flag_seq;
+  st.seq = next_seq(ctx->flag_seq);
   st.slice_cols = slice_cols;
   st.nslices = nsl;
-  st.timeout_ticks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
+  st.timeout_ticks = ctx->stream_timeout_ticks;  // default 1 s of s_memrealtime (100 MHz)
   uint32_t tiles[kMaxStreamSlices] = {};
   for (uint32_t i = 0; i < nsl; i++) {
     const uint32_t len = std::min(slice_cols, cols - i * slice_cols);
@@ -238,8 +243,14 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
     range(i, off, cnt);
     TMARK("pack");
     pack(off, cnt);
+    if (i == ctx->test_stall_slice && ctx->test_stall_calls > 0) {
+      // test knob: the host descheduled past the device's wait
+      ctx->test_stall_calls--;
+      std::this_thread::sleep_for(std::chrono::microseconds(ctx->test_stall_us));
+    }
     __atomic_store_n(ready_h + 16 * i, st.seq, __ATOMIC_RELEASE);
   }
+  if (during) (*during)();  // host work that overlaps the kernel
   bool ok = true;
   for (uint32_t i = 0; i < nsl && ok; i++) {
     TMARK("wait");
@@ -249,7 +260,8 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
       __builtin_ia32_pause();
 #endif
       if ((it & 1023) == 0 &&
-          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
+          std::chrono::steady_clock::now() - t0 >
+              std::chrono::milliseconds(ctx->stream_host_wait_ms)) {
         // the GPU may just be busy with other streams' work: drain, look again
         HIP_TRY(ctx, hipStreamSynchronize(s));
         ok = __atomic_load_n(done_h + 16 * i, __ATOMIC_ACQUIRE) == st.seq;
@@ -268,9 +280,11 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
     HIP_TRY(ctx, hipMemsetAsync(ctx->scnt.p, 0, kMaxStreamSlices * sizeof(uint32_t), s));
     HIP_TRY(ctx, hipStreamSynchronize(s));
     std::memset(ctx->sbase, 0, sizeof(ctx->sbase));
+    ctx->n_stream_fallbacks++;
     return kNotStreamed;
   }
   for (uint32_t i = 0; i < nsl; i++) ctx->sbase[i] += tiles[i];
+  ctx->n_streamed++;
   return STORB_RS_OK;
 }
 
@@ -279,20 +293,42 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
 
 extern "C" {
 
+// data_out (storb_rs_encode_shares; null for storb_rs_encode): the k data
+// shares are written too, B bytes each, the last one zero-padded -- what
+// zfec-rs Fec::encode returns beside the parity (piece.rs:329). Those copies
+// run on the host pool while the kernel works on the parity.
 static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
-                    size_t len, uint8_t *const *parity_out, size_t *block_out,
-                    size_t *padlen_out) {
+                      size_t len, uint8_t *const *parity_out, size_t *block_out,
+                      size_t *padlen_out, uint8_t *const *data_out = nullptr) {
   if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
   if (len == 0 || !data) return fail(ctx, STORB_RS_EINVAL, "empty chunk");
   const size_t B = (len + k - 1) / k, pad = B * k - len;
   if (block_out) *block_out = B;
   if (padlen_out) *padlen_out = pad;
   const uint32_t p = n - k;
-  if (p == 0) return STORB_RS_OK;
+  if (data_out)
+    for (uint32_t j = 0; j < k; j++)
+      if (!data_out[j]) return fail(ctx, STORB_RS_EINVAL, "null share output");
+  std::vector<CopySeg> dsegs;
+  if (data_out)
+    for (uint32_t j = 0; j < k; j++) {
+      const size_t src = static_cast<size_t>(j) * B;
+      const size_t avail = src < len ? std::min(B, len - src) : 0;
+      if (avail) dsegs.push_back({data_out[j], data + src, avail});
+      if (B > avail) dsegs.push_back({data_out[j] + avail, nullptr, B - avail});
+    }
+  const std::function<void()> put_data = [&] {
+    if (!dsegs.empty()) host_pool(ctx).copy_segs(dsegs.data(), dsegs.size());
+  };
+  if (p == 0) {
+    put_data();
+    return STORB_RS_OK;
+  }
   if (!parity_out) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
   for (uint32_t i = 0; i < p; i++)
     if (!parity_out[i]) return fail(ctx, STORB_RS_EINVAL, "null parity_out");
   if (k == 1) {
+    put_data();
     // Storb sizes every chunk <= 64 KiB (objects < 256 KiB) k = 1, m = 2
     // (piece.rs:307-317). Every generator row is then [1] -- a single data
     // share's Vandermonde column is all ones -- so each parity share IS the
@@ -357,9 +393,10 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       for (uint32_t i = 0; i < p; i++) out[i] = pd[i] + off;
       return encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), cnt, 1, s);
     };
-    if (in_direct && out_direct) {  // nothing to overlap
+    if (in_direct && out_direct) {  // nothing to overlap but the data shares
       const int rc = launch(0, S);
       if (rc) return rc;
+      put_data();
       HIP_TRY(ctx, hipStreamSynchronize(s));
       return STORB_RS_OK;
     }
@@ -374,10 +411,10 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       std::vector<const uint8_t *> sin(k);
       for (uint32_t j = 0; j < k; j++) sin[j] = dd + static_cast<size_t>(j) * S;
       const int rs = streamed(ctx, k, p, enc.data() + static_cast<size_t>(k) * k, sin.data(),
-                              pd.data(), S, pk, up, n);
+                              pd.data(), S, pk, up, n, data_out ? &put_data : nullptr);
       if (rs != kNotStreamed) return rs;
     }
-    return sliced(ctx, S, pk, launch, up);
+    return sliced(ctx, S, pk, launch, up, data_out ? &put_data : nullptr);
   }
   pack(0, S);
   uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
@@ -389,6 +426,7 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   if (rc) return rc;
   HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dp, static_cast<size_t>(p) * S,
                               hipMemcpyDeviceToHost, s));
+  put_data();
   HIP_TRY(ctx, hipStreamSynchronize(s));
   unpack(0, S);
   return STORB_RS_OK;
@@ -509,7 +547,7 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       const int rs = streamed(ctx, k, e, coef.data(), sin.data(), od.data(), S, pack, unpack);
       if (rs != kNotStreamed) return rs;
     }
-    return sliced(ctx, S, pack, launch, unpack);
+    return sliced(ctx, S, pack, launch, unpack, nullptr);
   }
   pack(0, S);
   uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
@@ -585,6 +623,18 @@ int storb_rs_encode(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *da
   if (!ctx) return STORB_RS_EINVAL;
   std::lock_guard<std::mutex> lk(ctx->mu);
   const int rc = encode_one(ctx, k, n, data, len, parity_out, block_out, padlen_out);
+  if (rc) drain_streams(ctx);  // queued work may still touch caller buffers
+  return rc;
+}
+
+int storb_rs_encode_shares(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
+                           size_t len, uint8_t *const *shares_out, size_t *block_out,
+                           size_t *padlen_out) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!shares_out) return fail(ctx, STORB_RS_EINVAL, "null shares_out");
+  const int rc = encode_one(ctx, k, n, data, len, valid_params(k, n) ? shares_out + k : nullptr,
+                            block_out, padlen_out, valid_params(k, n) ? shares_out : nullptr);
   if (rc) drain_streams(ctx);  // queued work may still touch caller buffers
   return rc;
 }

@@ -71,7 +71,10 @@ struct Tune {
   static constexpr int T = 256;
   static constexpr int U = 1;
   static constexpr bool BAR = false;
-  static constexpr int G = KM < 8 ? KM : 8;
+  // k = 32 with up to 4 rows: 4 shares per group (tools/k32_tune.hip,
+  // profiles/r3zb_k32_tune.txt, config 6 geometry, bit-exact): R = 1 74.0 ->
+  // 77.8 %, R = 2 63.9 -> 72.8 %, R = 4 54.3 -> 59.6 % of 8 TB/s against 8.
+  static constexpr int G = KM < 8 ? KM : (KM == 32 && RM <= 4 ? 4 : 8);
   static constexpr bool TL = KM >= 8;
   static constexpr bool PAIR = KM == 8 && RM <= 4;  // measured +2.5 % (W2)
 };

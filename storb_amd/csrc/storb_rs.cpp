@@ -490,6 +490,7 @@ const char *storb_rs_strerror(int code) {
     case STORB_RS_ENODEV: return "no usable gfx950 device";
     case STORB_RS_EAGAIN: return "async op still running";
     case STORB_RS_EBUSY: return "too many unfinished async ops on the context";
+    case STORB_RS_ECLOSED: return "the async op's context was destroyed before the op was finished";
     default: return "unknown error";
   }
 }
@@ -520,6 +521,18 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   if (const char *e = std::getenv("STORB_RS_ZC_BATCH")) c->zc_batch = std::atoi(e) != 0;
   if (const char *e = std::getenv("STORB_RS_TABLE_CACHE"))
     c->table_cap = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
+  if (const char *e = std::getenv("STORB_RS_TEST_STREAM_STALL")) {
+    unsigned long long ticks = 0, us = 0;
+    unsigned host_ms = 0, slice = 0, calls = 1;
+    if (std::sscanf(e, "%llu,%u,%u,%llu,%u", &ticks, &host_ms, &slice, &us, &calls) >= 4 &&
+        ticks > 0) {
+      c->stream_timeout_ticks = ticks;
+      c->stream_host_wait_ms = static_cast<int>(std::max(1u, host_ms));
+      c->test_stall_slice = slice;
+      c->test_stall_us = static_cast<uint32_t>(std::min<unsigned long long>(us, 5000000ull));
+      c->test_stall_calls = calls;
+    }
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->pipe[1], hipStreamNonBlocking) != hipSuccess) {
@@ -538,6 +551,19 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     for (auto &kv : ctx->tables) (void)release_table(ctx, kv.second.get());
     (void)hipStreamSynchronize(ctx->stream);
   }
+  // A table whose stream-ordered release failed: free it once nothing on the
+  // device can still read it (hipFree of pool memory after a device-wide
+  // synchronisation returns it to its pool).
+  bool leftover = false;
+  for (auto &kv : ctx->tables) leftover = leftover || kv.second->dev;
+  if (leftover) {
+    (void)hipDeviceSynchronize();
+    for (auto &kv : ctx->tables)
+      if (kv.second->dev) {
+        (void)hipFree(kv.second->dev);
+        kv.second->dev = nullptr;
+      }
+  }
   for (auto &p : ctx->pipe)
     if (p) (void)hipStreamSynchronize(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -555,12 +581,42 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
       (void)hipEventSynchronize(e);
       (void)hipEventDestroy(e);
     }
-  for (auto &sl : ctx->async_slots) {  // unfinished async ops: their work ends here
+  // Unfinished async ops: their device work ends here (the slot streams are
+  // drained below) and they are cut loose from the context, so a later
+  // storb_rs_op_test / _finish returns STORB_RS_ECLOSED without touching it.
+  invalidate_ops(ctx);
+  for (auto &sl : ctx->async_slots) {
     (void)hipStreamSynchronize(sl->stream);
     (void)hipStreamDestroy(sl->stream);
     (void)hipEventDestroy(sl->done);
   }
   delete ctx;  // frees tables, staging and pinned buffers on ctx->device
+}
+
+int storb_rs_device_pool_stats(int device, uint64_t *used, uint64_t *reserved) {
+  if (device < 0 || device >= storb_rs_device_count()) return STORB_RS_EINVAL;
+  DeviceGuard g(device);
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, device) != hipSuccess) return STORB_RS_EDEVICE;
+  uint64_t u = 0, r = 0;
+  if (hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &u) != hipSuccess ||
+      hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &r) != hipSuccess)
+    return STORB_RS_EDEVICE;
+  if (used) *used = u;
+  if (reserved) *reserved = r;
+  return STORB_RS_OK;
+}
+
+int storb_rs_ctx_stats(const storb_rs_ctx *ctx, storb_rs_ctx_stats_t *out) {
+  if (!ctx || !out) return STORB_RS_EINVAL;
+  out->streamed_calls = ctx->n_streamed.load();
+  out->stream_fallbacks = ctx->n_stream_fallbacks.load();
+  out->sliced_calls = ctx->n_sliced.load();
+  storb_rs_ctx *c = const_cast<storb_rs_ctx *>(ctx);
+  std::lock_guard<std::mutex> lk(c->async_mu);
+  out->live_ops = c->live_ops.size();
+  out->tables = ctx->tables.size();
+  return STORB_RS_OK;
 }
 
 int storb_rs_ctx_device(const storb_rs_ctx *ctx) { return ctx ? ctx->device : -1; }
@@ -628,6 +684,21 @@ int storb_rs_host_alloc(size_t len, void **out) {
   return STORB_RS_OK;
 }
 
+// hipHostFree / hipHostUnregister wait only for the null stream of each
+// device; the zero-copy kernels run on non-blocking streams (the contexts'
+// own, async slots, callers'), so a range could be unmapped under a kernel
+// still reading or writing it -- a GPU page fault reported later, against
+// whatever HIP call comes next. Every device is synchronised first. These
+// calls are rare (buffer teardown); the cost is one device-wide wait.
+static void sync_all_devices() {
+  int n = 0, prev = -1;
+  if (hipGetDeviceCount(&n) != hipSuccess) return;
+  (void)hipGetDevice(&prev);
+  for (int d = 0; d < n; d++)
+    if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
+
 int storb_rs_host_free(void *p) {
   if (!p) return STORB_RS_OK;
   {
@@ -636,6 +707,7 @@ int storb_rs_host_free(void *p) {
     if (it == g_pinned.end() || !it->second.second) return STORB_RS_EINVAL;
     g_pinned.erase(it);
   }
+  sync_all_devices();
   return hipHostFree(p) == hipSuccess ? STORB_RS_OK : STORB_RS_EDEVICE;
 }
 
@@ -658,6 +730,7 @@ int storb_rs_host_unregister(void *p) {
     if (it == g_pinned.end() || it->second.second) return STORB_RS_EINVAL;
     g_pinned.erase(it);
   }
+  sync_all_devices();
   return hipHostUnregister(p) == hipSuccess ? STORB_RS_OK : STORB_RS_EDEVICE;
 }
 

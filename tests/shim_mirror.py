@@ -3,7 +3,7 @@
 TEST INFRASTRUCTURE. The Rust crate cannot be compiled in this image (no
 cargo / rustc), so its logic is restated here statement for statement and run
 against a *backend* with the C ABI's contract (include/storb_rs.h
-storb_rs_block_size / storb_rs_encode / storb_rs_decode, return codes 0 / 1 / 2):
+storb_rs_block_size / storb_rs_encode_shares / storb_rs_decode, return codes 0 / 1 / 2):
 
 * `LibBackend` -- the real libstorb_rs.so through ctypes (needs a gfx950 GPU);
 * `OracleBackend` -- the CPU oracle (oracle/coracle.py) wrapped in that same
@@ -47,13 +47,13 @@ class OracleBackend:
     def check_params(self, k: int, n: int) -> int:  # storb_rs_check_params
         return 0 if 1 <= k <= n <= 256 else EINVAL
 
-    def encode(self, k, n, data: bytes, parity_out: list) -> tuple[int, int, int]:
+    def encode_shares(self, k, n, data: bytes, shares_out: list) -> tuple[int, int, int]:
         from oracle import coracle
         if self.check_params(k, n) or len(data) == 0:
             return EINVAL, 0, 0
         shares, B, pad = coracle.encode(k, n, data)
-        for i, out in enumerate(parity_out):
-            out[:B] = shares[k + i].tobytes()
+        for i, out in enumerate(shares_out):
+            out[:B] = shares[i].tobytes()
         return 0, B, pad
 
     def decode(self, k, n, shares: list, idx: list, block: int, padlen: int, out) -> int:
@@ -72,7 +72,7 @@ class OracleBackend:
 
 
 class LibBackend:
-    """libstorb_rs.so through ctypes, exactly the eight externs of lib.rs:23-51."""
+    """libstorb_rs.so through ctypes, the externs lib.rs's Fec uses."""
 
     def __init__(self, ctx_handle):
         from storb_amd import _lib
@@ -85,13 +85,13 @@ class LibBackend:
     def check_params(self, k, n):
         return int(self.L.storb_rs_check_params(k, n))
 
-    def encode(self, k, n, data: bytes, parity_out: list):
+    def encode_shares(self, k, n, data: bytes, shares_out: list):
         buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
-        outs = [(C.c_uint8 * max(1, len(p))).from_buffer(p) for p in parity_out]
+        outs = [(C.c_uint8 * max(1, len(p))).from_buffer(p) for p in shares_out]
         ptrs = (C.c_void_p * max(1, len(outs)))(*[C.addressof(o) for o in outs])
         b, pad = C.c_size_t(), C.c_size_t()
-        rc = self.L.storb_rs_encode(self.ctx, k, n, C.addressof(buf), len(data), ptrs,
-                                    C.byref(b), C.byref(pad))
+        rc = self.L.storb_rs_encode_shares(self.ctx, k, n, C.addressof(buf), len(data), ptrs,
+                                           C.byref(b), C.byref(pad))
         return int(rc), int(b.value), int(pad.value)
 
     def decode(self, k, n, shares, idx, block, padlen, out):
@@ -113,22 +113,18 @@ class Fec:
         self.k, self.m, self.be = k, m, backend
 
     def encode(self, data: bytes) -> tuple[list[Chunk], int]:
-        """lib.rs:142-163: m zeroed Vecs of b bytes, the k data shares sliced
-        out of `data` (the tail of the last one stays zero), parity written by
-        storb_rs_encode; returns all m shares in index order and padlen."""
+        """lib.rs Fec::encode: m Vecs of capacity b (uninitialised in Rust;
+        here filled with 0xCD so an unwritten byte shows), every share --
+        data shares zero-padded, then parity -- written by one
+        storb_rs_encode_shares call; returns all m shares in index order and
+        padlen."""
         k, m = self.k, self.m
         b = self.be.block_size(k, len(data))
-        chunks = [Chunk(bytearray(b), i) for i in range(m)]
-        for j in range(k):
-            off = j * b
-            if off < len(data):
-                end = min(off + b, len(data))
-                chunks[j].data[:end - off] = data[off:end]
-        parity = [c.data for c in chunks[k:]]
-        rc, _block, pad = self.be.encode(k, m, bytes(data), parity)
+        bufs = [bytearray(b"\xcd" * b) for _ in range(m)]
+        rc, _block, pad = self.be.encode_shares(k, m, bytes(data), bufs)
         if rc != 0:
             raise ShimError(rc)
-        return chunks, pad
+        return [Chunk(bufs[i], i) for i in range(m)], pad
 
     def decode(self, encoded_data: list[Chunk], padding: int) -> bytes:
         """lib.rs:166-186: Err(2) below k shares; b from the first share; Err(1)
@@ -140,7 +136,7 @@ class Fec:
         b = len(encoded_data[0].data)
         if b == 0 or padding >= k * b or any(len(c.data) != b for c in encoded_data):
             raise ShimError(EINVAL)
-        out = bytearray(k * b - padding)
+        out = bytearray(b"\xcd" * (k * b - padding))  # Vec::with_capacity: not zero-filled
         rc = self.be.decode(k, self.m, [c.data for c in encoded_data],
                             [c.index for c in encoded_data], b, padding, out)
         if rc != 0:

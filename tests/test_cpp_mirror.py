@@ -43,3 +43,15 @@ def test_host_pool_copies_and_runs_every_part():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "host pool ok" in r.stdout
+
+
+def test_sequence_numbers_skip_zero_across_the_wrap():
+    """the slice words start zeroed, so a sequence number of 0
+    would match a never-written word after 2^32 calls (storb_amd/csrc/seq.hpp)."""
+    src = os.path.join(ROOT, "tests", "cpp", "test_seq.cpp")
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "test_seq")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, src], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "seq ok" in r.stdout

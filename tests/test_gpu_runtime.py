@@ -145,3 +145,55 @@ def test_host_register_direct_paths():
     interior offsets by encode, decode and encode_chunks; oracle-exact. Runs
     in a child process (tests/registered_ranges.py)."""
     run_registered_case("direct_paths")
+
+
+def test_streamed_call_gives_up_resets_and_streams_again(monkeypatch):
+    """the streamed single call's give-up path, forced.
+
+    The test knob (read once per context, storb_amd/csrc/ctx.hpp) makes a
+    workgroup wait at most 20 ms (2,000,000 s_memrealtime ticks) for its
+    slice's ready word and the host at most 200 ms for a done word, and makes
+    the host sleep 100 ms before publishing slice 1 in the first streamed call
+    -- a host descheduled past the device's wait. Slice 1's workgroups give up
+    and exit without writing; the host drains the stream, resets the slice
+    counters and redoes the call on the sliced path (host_calls.cpp streamed).
+    The result must equal the oracle's, and the next calls must stream again
+    (the counters were reset: a stale count would leave a done word unset)."""
+    monkeypatch.setenv("STORB_RS_TEST_STREAM_STALL", "2000000,200,1,100000,1")
+    ctx = _lib.Context(0)
+    monkeypatch.delenv("STORB_RS_TEST_STREAM_STALL")
+    try:
+        k, n = 4, 6
+        data = rnd(1 << 20, 31)  # B = 256 KiB: 4 slices of 64 KiB per share
+        want, B, pad = coracle.encode(k, n, data)
+        got, b, p = ctx.encode(k, n, data)
+        assert (b, p) == (B, pad)
+        assert got == [bytes(w) for w in want[k:]]
+        st = ctx.stats()
+        assert st["stream_fallbacks"] == 1 and st["sliced_calls"] == 1, st
+        assert st["streamed_calls"] == 0, st
+        for seed in (32, 33):  # streams again, exact
+            d = rnd(1 << 20, seed)
+            assert ctx.encode(k, n, d)[0] == [bytes(w) for w in coracle.encode(k, n, d)[0][k:]]
+        shares = [bytes(w) for w in want]
+        idx = [2, 3, 4, 5]
+        assert ctx.decode(k, n, [shares[i] for i in idx], idx, B, pad) == data.tobytes()
+        st = ctx.stats()
+        assert st["stream_fallbacks"] == 1 and st["streamed_calls"] == 3, st
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("k,n,L", [(4, 6, 1 << 20), (4, 6, (1 << 20) - 5), (2, 3, 256 << 10),
+                                   (16, 24, 8 << 20), (8, 12, 3 << 20 | 17), (1, 2, 4097),
+                                   (3, 3, 1000), (32, 48, 32 << 20)])
+def test_encode_shares_all_n_shares_match_oracle(ctx, k, n, L):
+    """storb_rs_encode_shares: every share of zfec-rs Fec::encode's result
+    (piece.rs:329) -- data shares zero-padded, then parity -- from one call,
+    the data shares copied by the host pool while the kernel runs."""
+    data = rnd(L, 40 + k)
+    want, B, pad = coracle.encode(k, n, data)
+    got, b, p = ctx.encode_shares(k, n, data)
+    assert (b, p) == (B, pad)
+    for i in range(n):
+        assert got[i].tobytes() == bytes(want[i]), i

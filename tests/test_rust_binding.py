@@ -22,14 +22,16 @@ import pytest
 import shim_mirror as S
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_RS = os.path.join(ROOT, "integration", "zfec-rs-mi355x", "src", "lib.rs")
+CRATE_SRC = os.path.join(ROOT, "integration", "zfec-rs-mi355x", "src")
+LIB_RS = os.path.join(CRATE_SRC, "lib.rs")
+MI355X_RS = os.path.join(CRATE_SRC, "mi355x.rs")
 HEADER = os.path.join(ROOT, "include", "storb_rs.h")
 GOLDEN = os.path.join(ROOT, "tests", "golden", "zfec_vectors.json")
 
 C_BASE = {"int": "c_int", "uint32_t": "u32", "size_t": "usize", "uint8_t": "u8",
           "char": "c_char", "uint64_t": "u64", "void": "c_void",
           "storb_rs_ctx": "StorbRsCtx", "storb_rs_op": "StorbRsOp",
-          "storb_rs_jit_stats_t": "StorbRsJitStats",
+          "storb_rs_jit_stats_t": "StorbRsJitStats", "storb_rs_ctx_stats_t": "StorbRsCtxStats",
           "storb_rs_notify_fn": 'Option<unsafe extern "C" fn(*mut c_void)>'}
 
 
@@ -78,17 +80,21 @@ def header_prototypes() -> dict:
     return protos
 
 
-def rust_externs() -> dict:
-    src = open(LIB_RS).read()
-    block = re.search(r'extern "C" \{(.*?)\n\}', src, re.S).group(1)
+def rust_externs(path=LIB_RS) -> dict:
+    """Every storb_* function of every `extern "C"` block of one source file
+    (the glibc eventfd/close block of mi355x.rs is not the ABI's)."""
+    src = open(path).read()
     out = {}
-    for m in re.finditer(r"fn\s+(\w+)\s*\((.*?)\)\s*(->\s*([^;]+))?;", block, re.S):
-        name, params, ret = m.group(1), m.group(2), m.group(4)
-        plist = []
-        for p in [x.strip() for x in params.split(",") if x.strip()]:
-            _, ty = p.split(":", 1)
-            plist.append(" ".join(ty.split()))
-        out[name] = (ret.strip() if ret else None, plist)
+    for block in re.findall(r'extern "C" \{(.*?)\n\}', src, re.S):
+        for m in re.finditer(r"fn\s+(\w+)\s*\((.*?)\)\s*(->\s*([^;]+))?;", block, re.S):
+            name, params, ret = m.group(1), m.group(2), m.group(4)
+            if not name.startswith("storb_"):
+                continue
+            plist = []
+            for p in [x.strip() for x in params.split(",") if x.strip()]:
+                _, ty = p.split(":", 1)
+                plist.append(" ".join(ty.split()))
+            out[name] = (ret.strip() if ret else None, plist)
     return out
 
 
@@ -102,11 +108,8 @@ def test_c_type_mapping_rules():
     assert c_type_to_rust("const char *") == "*const c_char"
 
 
-def test_every_rust_extern_matches_the_header():
+def _check_against_header(rs):
     hdr = header_prototypes()
-    rs = rust_externs()
-    assert len(rs) == 8, sorted(rs)  # lib.rs:23-51 binds exactly these eight
-    assert {"storb_rs_encode", "storb_rs_decode", "storb_rs_ctx_create"} <= set(rs)
     for name, (ret, params) in rs.items():
         assert name in hdr, f"{name} is not declared in include/storb_rs.h"
         hret, hparams = hdr[name]
@@ -114,6 +117,30 @@ def test_every_rust_extern_matches_the_header():
         for i, (r, h) in enumerate(zip(params, hparams)):
             assert r == h, f"{name} parameter {i}: Rust {r!r} vs header {h!r}"
         assert ret == hret, f"{name} return: Rust {ret!r} vs header {hret!r}"
+
+
+def test_every_rust_extern_matches_the_header():
+    rs = rust_externs(LIB_RS)
+    # the zfec-rs API (Fec::new / encode / decode) binds exactly these eight
+    assert set(rs) == {"storb_rs_ctx_create", "storb_rs_ctx_destroy", "storb_rs_strerror",
+                       "storb_rs_last_error", "storb_rs_check_params", "storb_rs_block_size",
+                       "storb_rs_encode_shares", "storb_rs_decode"}, sorted(rs)
+    _check_against_header(rs)
+
+
+def test_mi355x_module_externs_match_the_header():
+    """the batch, hashed, async and page-locked calls an
+    integrator wires into upload.rs:418-420 / download.rs:464 have a pinned
+    Rust surface (zfec_rs::mi355x)."""
+    rs = rust_externs(MI355X_RS)
+    want = {"storb_rs_encode_chunks", "storb_rs_encode_chunks_hashed", "storb_rs_decode_chunks",
+            "storb_rs_encode_async", "storb_rs_decode_async", "storb_rs_op_test",
+            "storb_rs_op_finish", "storb_rs_notify_fd", "storb_rs_host_alloc",
+            "storb_rs_host_free", "storb_rs_host_register", "storb_rs_host_unregister",
+            "storb_blake3"}
+    assert want <= set(rs), sorted(want - set(rs))
+    _check_against_header(rs)
+    assert "pub mod mi355x;" in open(LIB_RS).read()
 
 
 def test_header_parser_sees_the_whole_abi():
@@ -179,7 +206,7 @@ def test_shim_checks_cpu():
     with pytest.raises(S.ShimError) as e:  # b == 0
         fec.decode([S.Chunk(bytearray(), i) for i in range(4)], 0)
     assert e.value.code == S.EINVAL
-    with pytest.raises(S.ShimError) as e:  # empty chunk: storb_rs_encode EINVAL
+    with pytest.raises(S.ShimError) as e:  # empty chunk: storb_rs_encode_shares EINVAL
         fec.encode(b"")
     assert e.value.code == S.EINVAL
 

@@ -8,9 +8,8 @@
 // interleaved rounds (median of reps, HIP events on one stream).
 // Bytes = nstripes x (k + R) x B.
 //
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Istorb_amd/csrc tools/k32_tune.hip \
-//          -o tools/_build/k32_tune
-// usage: k32_tune [REPS]
+// build: make -C tools k32_tune
+// usage: k32_tune [REPS] [ALL]: R = 3, 5, 6, 8, 16 (round 4); ALL = 1 adds R = 1, 2, 4
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,6 +44,24 @@ struct Var {
 template <int R>
 std::vector<Var> variants() {
   std::vector<Var> v;
+  if constexpr (R > 4 || R == 3) {  // the round-4 sweep of the remaining row buckets
+    v.push_back({"r3 product U1 G8 TL", [](const ApplyArgs &a, hipStream_t s) {
+                   return launch_perm<32, R, 256, 1, false, 8, true>(a, s, 0);
+                 }});
+    v.push_back({"U1 G4 TL", [](const ApplyArgs &a, hipStream_t s) {
+                   return launch_perm<32, R, 256, 1, false, 4, true>(a, s, 0);
+                 }});
+    v.push_back({"U1 G2 TL", [](const ApplyArgs &a, hipStream_t s) {
+                   return launch_perm<32, R, 256, 1, false, 2, true>(a, s, 0);
+                 }});
+    v.push_back({"U1 G16 TL", [](const ApplyArgs &a, hipStream_t s) {
+                   return launch_perm<32, R, 256, 1, false, 16, true>(a, s, 0);
+                 }});
+    v.push_back({"U1 G4 TL cap4", [](const ApplyArgs &a, hipStream_t s) {
+                   return launch_perm<32, R, 256, 1, false, 4, true>(a, s, 4);
+                 }});
+    return v;
+  }
   v.push_back({"product U1 G8 TL", [](const ApplyArgs &a, hipStream_t s) {
                  return launch_perm<32, R, 256, 1, false, 8, true>(a, s, Tune<32, R>::OCC);
                }});
@@ -156,15 +173,20 @@ int main(int argc, char **argv) {
   PermTab *dt;
   CK(hipMalloc(&d, N * k * B));
   CK(hipMalloc(&p, N * 16 * B));
-  CK(hipMalloc(&o, N * 4 * B));
-  CK(hipMalloc(&dt, k * 4 * sizeof(PermTab)));
+  CK(hipMalloc(&o, N * 16 * B));
+  CK(hipMalloc(&dt, k * 16 * sizeof(PermTab)));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(d),
                      N * k * B / 8, 11);
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(p),
                      N * 16 * B / 8, 12);
   CK(hipDeviceSynchronize());
-  if (run<1>(reps, d, p, o, dt, N, B) || run<2>(reps, d, p, o, dt, N, B) ||
-      run<4>(reps, d, p, o, dt, N, B))
+  const bool all = argc > 2 && std::atoi(argv[2]) == 1;  // 1: R = 1, 2, 4 too (round 3's sweep)
+  if (all && (run<1>(reps, d, p, o, dt, N, B) || run<2>(reps, d, p, o, dt, N, B) ||
+              run<4>(reps, d, p, o, dt, N, B)))
+    return 1;
+  if (run<3>(reps, d, p, o, dt, N, B) || run<5>(reps, d, p, o, dt, N, B) ||
+      run<6>(reps, d, p, o, dt, N, B) || run<8>(reps, d, p, o, dt, N, B) ||
+      run<16>(reps, d, p, o, dt, N, B))
     return 1;
   return 0;
 }
