@@ -301,8 +301,10 @@ int storb_rs_decode_stripes_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   // Assembly into a separate buffer: stored by the kernel from its own loads
   // for k <= kCopyMaxK; wider codes copy all data slots first (one 2-D copy)
   // and rebuild the missing rows over them.
+  // (With no surviving data share in any stripe -- possible when n >= 2k --
+  // every data row is rebuilt and d_data may be null: nothing to copy.)
   const bool fused = assemble && k <= kCopyMaxK;
-  if (assemble && !fused)
+  if (assemble && !fused && need_data)
     HIP_TRY(ctx, hipMemcpy2DAsync(d_out, out_stride, d_data, data_stride,
                                   static_cast<size_t>(k) * block, nstripes,
                                   hipMemcpyDeviceToDevice, s));

@@ -123,7 +123,7 @@ rs_encode_bitslice(const ApplyArgs a) {
 }
 
 // The row-split form for geometries bs_split leaves to one wave per tile
-// (A/B: STORB_RS_BS_SPLIT=1, rs_bitslice.hip). CAP resident per CU.
+// (the round-2 A/B of it at k = 16 / 32 is in DESIGN.md §4). CAP resident per CU.
 template <int K, int N, int CAP>
 __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(2))) void
 rs_encode_bitslice_split(const ApplyArgs a) {

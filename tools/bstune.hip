@@ -22,8 +22,6 @@
 
 using namespace storb_rs;
 
-int storb_rs::wg_cap_override() { return -1; }
-int storb_rs::table_threads_override() { return 0; }
 
 #define CK(x)                                                                  \
   do {                                                                         \

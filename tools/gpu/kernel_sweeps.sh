@@ -11,5 +11,5 @@ timeout -k 10 120 tools/_build/mixbench 25 32 > $O/mixbench32.txt 2>&1 && cat $O
 timeout -k 10 240 tools/_build/k32_tune 15 > $O/k32_tune.txt 2>&1 && cat $O/k32_tune.txt &&
 timeout -k 10 120 tools/_build/descbench 20 32 > $O/descbench32.txt 2>&1 && cat $O/descbench32.txt &&
 timeout -k 10 120 tools/_build/descbench 20 16 > $O/descbench16.txt 2>&1 && cat $O/descbench16.txt &&
-timeout -k 10 400 python -u -m pytest tests/test_gpu_patterns.py tests/test_gpu_jit.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_lifetime.py tests/test_gpu_runtime.py tests/test_gpu_patterns.py tests/test_gpu_async.py tests/test_gpu_jit.py -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 tail -3 $O/tests.log; exit $rc

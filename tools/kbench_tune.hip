@@ -24,10 +24,6 @@
 
 using namespace storb_rs;
 
-// The product reads STORB_RS_WG_PER_CU here (rs_kernels.hip); this tool
-// sets every cap itself.
-int storb_rs::wg_cap_override() { return -1; }
-int storb_rs::table_threads_override() { return 0; }
 
 #define CK(x)                                                                  \
   do {                                                                         \

@@ -56,10 +56,20 @@ struct Bounds {
 
 typedef const PermTab __attribute__((address_space(4))) cPermTab;
 
-template <int KM, int R, int G, bool TL, bool INL>
+// Shares per load group of the branch with R rows: GSET 0 = G everywhere;
+// 1 = k = 32 {16, 16, 2, 4} / k = 16 {8, 8, 4, 4}; 2 = k = 32 {16, 16, 4, 4}
+// / k = 16 {16, 8, 8, 8}.
+template <int KM, int G, int GSET>
+constexpr int gsel(int R) {
+  if (GSET == 1) return KM == 32 ? (R <= 2 ? 16 : R == 3 ? 2 : 4) : (R <= 2 ? 8 : 4);
+  if (GSET == 2) return KM == 32 ? (R <= 2 ? 16 : 4) : (R == 1 ? 16 : 8);
+  return G;
+}
+
+template <int KM, int R, int G, bool TL, bool INL, int U = 1>
 __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *rec,
                                       PermTab *lds) {
-  constexpr uint32_t TILE = kThreads;
+  constexpr uint32_t TILE = kThreads * U;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + TILE - 1) / TILE;
   const uint32_t t = blockIdx.x % tps;
@@ -68,16 +78,16 @@ __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *
   const uint32_t base = t * TILE;
   auto go = [&](auto tabs) {
     if (base + TILE <= cols)
-      perm_tile<KM, R, TILE, 1, false, G, false, false, false>(v, tabs, a.k, R, cols,
-                                                             base + threadIdx.x);
+      perm_tile<KM, R, kThreads, U, false, G, false, false, false>(v, tabs, a.k, R, cols,
+                                                                 base + threadIdx.x);
     else
-      perm_tile<KM, R, TILE, 1, false, G, false, true, false>(v, tabs, a.k, R, cols,
-                                                            base + threadIdx.x);
+      perm_tile<KM, R, kThreads, U, false, G, false, true, false>(v, tabs, a.k, R, cols,
+                                                                base + threadIdx.x);
   };
   if constexpr (TL) {
     typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
     const uint32_t n16 = a.k * R * (sizeof(PermTab) / 16);
-    for (uint32_t i = threadIdx.x; i < n16; i += TILE)
+    for (uint32_t i = threadIdx.x; i < n16; i += kThreads)
       reinterpret_cast<u32x4 *>(lds)[i] = ((gcu32x4 *)(gt))[i];
     __syncthreads();
     go(static_cast<const PermTab *>(lds));
@@ -86,10 +96,10 @@ __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *
   }
 }
 
-template <int KM, int G, bool TL, bool SORTED, bool INL>
+template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0>
 __global__ __launch_bounds__(kThreads) void mixv(const DescArgs a, const Bounds b) {
   __shared__ __attribute__((aligned(16))) PermTab lds[TL ? KM * kMixR : 1];
-  const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + kThreads - 1) / kThreads;
+  const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + kThreads * U - 1) / (kThreads * U);
   const uint32_t item = blockIdx.x / tps;
   cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
   uint32_t r;
@@ -97,10 +107,10 @@ __global__ __launch_bounds__(kThreads) void mixv(const DescArgs a, const Bounds 
     r = blockIdx.x >= b.first[4] ? 4 : blockIdx.x >= b.first[3] ? 3 : blockIdx.x >= b.first[2] ? 2 : 1;
   else
     r = static_cast<uint32_t>(rec[0] >> 32);
-  if (r <= 1) return vbody<KM, 1, G, TL, INL>(a, b, rec, lds);
-  if (r == 2) return vbody<KM, 2, G, TL, INL>(a, b, rec, lds);
-  if (r == 3) return vbody<KM, 3, G, TL, INL>(a, b, rec, lds);
-  return vbody<KM, 4, G, TL, INL>(a, b, rec, lds);
+  if (r <= 1) return vbody<KM, 1, gsel<KM, G, GSET>(1), TL, INL, U>(a, b, rec, lds);
+  if (r == 2) return vbody<KM, 2, gsel<KM, G, GSET>(2), TL, INL, U>(a, b, rec, lds);
+  if (r == 3) return vbody<KM, 3, gsel<KM, G, GSET>(3), TL, INL, U>(a, b, rec, lds);
+  return vbody<KM, 4, gsel<KM, G, GSET>(4), TL, INL, U>(a, b, rec, lds);
 }
 
 struct Var {
@@ -108,15 +118,17 @@ struct Var {
   bool sorted, inl;
   std::function<hipError_t(const DescArgs &, const Bounds &, hipStream_t)> fn;
   std::vector<float> ms;
+  int U = 1;
 };
 
-template <int KM, int G, bool TL, bool SORTED, bool INL>
+template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0>
 Var mk(const char *name, int cap) {
   return {name, SORTED, INL, [cap](const DescArgs &a, const Bounds &b, hipStream_t s) {
-            const uint64_t tps = ((a.block >> 4) + kThreads - 1) / kThreads;
+            const uint64_t tps = ((a.block >> 4) + kThreads * U - 1) / (kThreads * U);
             const size_t dyn = cap_lds(cap, TL ? sizeof(PermTab) * KM * kMixR : 0);
-            return launch_lds<mixv<KM, G, TL, SORTED, INL>>(tps * a.nitems, kThreads, dyn, s, a, b);
-          }, {}};
+            return launch_lds<mixv<KM, G, TL, SORTED, INL, U, GSET>>(tps * a.nitems, kThreads, dyn,
+                                                                     s, a, b);
+          }, {}, U};
 }
 
 template <int KM>
@@ -127,21 +139,22 @@ std::vector<Var> variants() {
                {}});
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
-  v.push_back(mk<KM, GP, false, false, false>("noTL", 0));
-  v.push_back(mk<KM, GP, true, true, false>("sorted TL", 0));
-  v.push_back(mk<KM, GP, false, true, false>("sorted noTL", 0));
-  v.push_back(mk<KM, GP, false, true, true>("sorted noTL inline", 0));
+  v.push_back(mk<KM, GP, true, false, false>("same shape cap2", 2));
+  v.push_back(mk<KM, GP, true, false, false>("same shape cap3", 3));
   v.push_back(mk<KM, GP, true, true, true>("sorted TL inline", 0));
-  v.push_back(mk<KM, GP, false, true, true>("sorted noTL inline cap4", 4));
-  v.push_back(mk<KM, 4, false, true, true>("sorted noTL inline G4", 0));
-  v.push_back(mk<KM, 4, true, false, false>("G4 (TL, rec[0])", 0));
-  v.push_back(mk<KM, 8, true, false, false>("G8 (TL, rec[0])", 0));
-  v.push_back(mk<KM, 8, false, true, true>("sorted noTL inline G8", 0));
+  v.push_back(mk<KM, GP, true, true, true>("sorted TL inline cap2", 2));
+  v.push_back(mk<KM, GP, true, true, true>("sorted TL inline cap3", 3));
+  v.push_back(mk<KM, GP, false, true, true>("sorted noTL inline cap2", 2));
+  v.push_back(mk<KM, GP, false, true, true>("sorted noTL inline cap3", 3));
+  v.push_back(mk<KM, 4, true, false, false, 2>("U2 G4 (TL, rec[0])", 0));
+  v.push_back(mk<KM, 4, true, false, false, 2>("U2 G4 cap2", 2));
+  v.push_back(mk<KM, 4, true, false, false, 2>("U2 G4 cap3", 3));
+  v.push_back(mk<KM, 4, true, true, true, 2>("U2 G4 sorted TL inline cap2", 2));
+  v.push_back(mk<KM, GP, true, false, false, 1, 1>("GSET1 (TL, rec[0])", 0));
+  v.push_back(mk<KM, GP, true, false, false, 1, 2>("GSET2 (TL, rec[0])", 0));
   if constexpr (KM == 32) {
-    v.push_back(mk<KM, 16, false, true, true>("sorted noTL inline G16", 0));
     v.push_back(mk<KM, 16, true, false, false>("G16 (TL, rec[0])", 0));
-  } else {
-    v.push_back(mk<KM, 2, false, true, true>("sorted noTL inline G2", 0));
+    v.push_back(mk<KM, 16, true, false, false>("G16 cap3", 3));
   }
   return v;
 }
@@ -206,8 +219,9 @@ int run(int reps) {
   const uint32_t tps = static_cast<uint32_t>((B / 16 + kThreads - 1) / kThreads);
   const uint32_t tab_q = 1 + k + kMixR;
   const uint32_t rec_plain = 1 + k + kMixR, rec_inl = tab_q + 4 * k * kMixR;
-  auto build = [&](bool sorted, bool inl, std::vector<uint64_t> &rec, std::vector<PermTab> &tab,
-                   Bounds &b) {
+  auto build = [&](bool sorted, bool inl, int U, std::vector<uint64_t> &rec,
+                   std::vector<PermTab> &tab, Bounds &b) {
+    const uint32_t tpsU = static_cast<uint32_t>((B / 16 + kThreads * U - 1) / (kThreads * U));
     std::vector<uint32_t> ord(items.size());
     for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
     if (sorted)
@@ -220,7 +234,7 @@ int run(int reps) {
     for (uint32_t q = 0; q < ord.size(); q++) {
       const Item &it = items[ord[q]];
       if (sorted && b.first[it.e] == UINT32_MAX)
-        for (uint32_t r = 1; r <= it.e; r++) b.first[r] = std::min(b.first[r], q * tps);
+        for (uint32_t r = 1; r <= it.e; r++) b.first[r] = std::min(b.first[r], q * tpsU);
       const size_t r0 = rec.size();
       rec.resize(r0 + (inl ? rec_inl : rec_plain), 0);
       rec[r0] = (inl ? 0 : tab.size()) | (uint64_t(it.e) << 32);
@@ -235,7 +249,7 @@ int run(int reps) {
     }
     // sorted: counts above the largest present start past the grid
     for (uint32_t r = 1; r <= kMixR; r++)
-      if (b.first[r] == UINT32_MAX) b.first[r] = static_cast<uint32_t>(ord.size()) * tps;
+      if (b.first[r] == UINT32_MAX) b.first[r] = static_cast<uint32_t>(ord.size()) * tpsU;
   };
   auto vs = variants<KM>();
   struct Up {
@@ -248,7 +262,7 @@ int run(int reps) {
   for (size_t vi = 0; vi < vs.size(); vi++) {
     std::vector<uint64_t> rec;
     std::vector<PermTab> tab;
-    build(vs[vi].sorted, vs[vi].inl, rec, tab, ups[vi].b);
+    build(vs[vi].sorted, vs[vi].inl, vs[vi].U, rec, tab, ups[vi].b);
     CK(hipMalloc(&ups[vi].rec, rec.size() * 8));
     CK(hipMemcpy(ups[vi].rec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice));
     CK(hipMalloc(&ups[vi].tab, std::max<size_t>(1, tab.size()) * sizeof(PermTab)));
@@ -300,6 +314,106 @@ int run(int reps) {
     const float m = v.ms[v.ms.size() / 2];
     std::printf("k=%u %-34s %8.4f ms  %6.2f TB/s  %5.1f %%  (bit-exact)\n", k, v.name.c_str(), m,
                 bytes / (m * 1e-3) / 1e12, 100.0 * bytes / (m * 1e-3) / 8e12);
+  }
+  // Isolation: only the chunks that lost 2 data shares, every one with the
+  // same survivor slots (lost data shares {0, 1}): the mixed-row kernel over
+  // them (records) against the uniform table kernel over the same stripes
+  // (pointers in kernel arguments), same tables.
+  {
+    std::vector<uint32_t> st2;
+    for (uint32_t s2 = 0; s2 < N; s2++)
+      if (es[s2] == 2) st2.push_back(s2);
+    std::vector<PermTab> tabs(k * 2);
+    for (auto &t : tabs) t = perm_tab(uint8_t(rng() | 1));
+    PermTab *dtab;
+    CK(hipMalloc(&dtab, tabs.size() * sizeof(PermTab)));
+    CK(hipMemcpy(dtab, tabs.data(), tabs.size() * sizeof(PermTab), hipMemcpyHostToDevice));
+    const uint32_t M = static_cast<uint32_t>(st2.size());
+    // the uniform launch needs equally spaced stripes: use the first M stripes
+    std::vector<uint64_t> rec;
+    for (uint32_t q = 0; q < M; q++) {
+      rec.push_back(0 | (uint64_t(2) << 32));
+      for (uint32_t c = 0; c < k; c++) {
+        const uint32_t id = c < 2 ? k + c : c;  // slots 0, 1 <- parity 0, 1
+        rec.push_back(reinterpret_cast<uint64_t>(id < k ? d + q * k * B + id * B
+                                                        : p + q * (n - k) * B + (id - k) * B));
+      }
+      for (uint32_t i = 0; i < kMixR; i++)
+        rec.push_back(i < 2 ? reinterpret_cast<uint64_t>(o + (size_t(q) * kMixR + i) * B) : 0);
+    }
+    uint64_t *drec;
+    CK(hipMalloc(&drec, rec.size() * 8));
+    CK(hipMemcpy(drec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice));
+    DescArgs da{};
+    da.desc = drec;
+    da.ptab = dtab;
+    da.block = B;
+    da.k = k;
+    da.r = kMixR;
+    da.tpw = 1;
+    da.nitems = M;
+    da.rec_qwords = 1 + k + kMixR;
+    da.mix = 1;
+    ApplyArgs aa{};
+    for (uint32_t c = 0; c < k; c++) {
+      const uint32_t id = c < 2 ? k + c : c;
+      aa.in[c] = id < k ? d + id * B : p + (id - k) * B;
+      aa.in_stride[c] = id < k ? k * B : (n - k) * B;
+    }
+    for (uint32_t i = 0; i < 2; i++) {
+      aa.out[i] = o + i * B;
+      aa.out_stride[i] = kMixR * B;
+    }
+    aa.ptab = dtab;
+    aa.k = k;
+    aa.r = 2;
+    aa.tab_rows = 2;
+    aa.block = B;
+    aa.nstripes = M;
+    using C2 = Tune<KM, 2>;
+    auto uni = [&](int cap) {
+      return launch_perm<KM, 2, C2::T, C2::U, C2::BAR, C2::G, C2::TL, C2::PAIR>(aa, s, cap);
+    };
+    struct Iso {
+      const char *name;
+      std::function<hipError_t()> fn;
+      std::vector<float> ms;
+    };
+    std::vector<Iso> iso = {
+        {"r=2 subset: mixed-row kernel (records)", [&] { return launch_apply_desc(da, s); }, {}},
+        {"r=2 subset: uniform rs_apply_perm, tuned cap", [&] { return uni(C2::OCC); }, {}},
+        {"r=2 subset: uniform rs_apply_perm, uncapped", [&] { return uni(0); }, {}},
+    };
+    std::vector<uint8_t> w2(ob), g2(ob);
+    for (size_t vi = 0; vi < iso.size(); vi++) {
+      CK(hipMemsetAsync(o, 0xEE, ob, s));
+      CK(iso[vi].fn());
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(vi ? g2.data() : w2.data(), o, ob, hipMemcpyDeviceToHost));
+      if (vi && std::memcmp(w2.data(), g2.data(), ob) != 0) {
+        std::printf("isolation %s: MISMATCH\n", iso[vi].name);
+        return 1;
+      }
+    }
+    for (int r = 0; r < reps; r++)
+      for (auto &v : iso) {
+        CK(hipEventRecord(e0, s));
+        CK(v.fn());
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float x = 0;
+        CK(hipEventElapsedTime(&x, e0, e1));
+        v.ms.push_back(x);
+      }
+    const double b2 = double(M) * (k + 2) * B;
+    for (auto &v : iso) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float m = v.ms[v.ms.size() / 2];
+      std::printf("k=%u %-44s %8.4f ms  %6.2f TB/s  %5.1f %%  (bit-exact, %u stripes)\n", k,
+                  v.name, m, b2 / (m * 1e-3) / 1e12, 100.0 * b2 / (m * 1e-3) / 8e12, M);
+    }
+    CK(hipFree(drec));
+    CK(hipFree(dtab));
   }
   CK(hipStreamDestroy(s));
   for (auto &u : ups) {
