@@ -140,10 +140,10 @@ def test_decode_stripes_dev_parity_only_survivors_null_data_region(ctx):
     """k > 16 decoded into a separate buffer with no surviving data
     share in any stripe (n >= 2k) and d_data = NULL -- every data row is
     rebuilt from parity, and nothing may be copied from the null region."""
-    k, n, B, ns = 17, 34, 4096, 6
+    k, n, B, ns = 17, 40, 4096, 6
     data, par = oracle_stripes(k, n, B, ns, 99)
-    sets = [list(range(k + s, k + s + k)) for s in range(ns)]  # a different parity window each
-    sets = [[k + ((i - k + s) % (n - k)) for i in range(k, 2 * k)] for s in range(ns)]
+    sets = [list(range(k + s, 2 * k + s)) for s in range(ns)]  # a different parity window each
+    assert len({tuple(x) for x in sets}) == ns
     dp = torch.from_numpy(par.copy()).to(DEV)
     out = torch.full((ns * k * B,), 0x3C, dtype=torch.uint8, device=DEV)
     ctx.decode_stripes_dev(k, n, B, sets, 0, dp.data_ptr(), out.data_ptr())
