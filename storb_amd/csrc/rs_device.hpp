@@ -64,6 +64,10 @@ constexpr int occ_for(int KM, int RM, bool copy) {
   return 0;
 }
 
+constexpr int g32(int RM) {
+  return RM <= 2 ? 16 : (RM == 3 || RM == 5 || RM == 6 || RM == 7) ? 2 : RM == 16 ? 8 : 4;
+}
+
 template <int KM, int RM>
 struct Tune {
   static constexpr int OCC = occ_for(KM, RM, false);
@@ -71,10 +75,13 @@ struct Tune {
   static constexpr int T = 256;
   static constexpr int U = 1;
   static constexpr bool BAR = false;
-  // k = 32 with up to 4 rows: 4 shares per group (tools/k32_tune.hip,
-  // profiles/r3zb_k32_tune.txt, config 6 geometry, bit-exact): R = 1 74.0 ->
-  // 77.8 %, R = 2 63.9 -> 72.8 %, R = 4 54.3 -> 59.6 % of 8 TB/s against 8.
-  static constexpr int G = KM < 8 ? KM : (KM == 32 && RM <= 4 ? 4 : 8);
+  // k = 32: shares per load group by row count (tools/k32_tune.hip, config 6
+  // geometry, every variant bit-exact against the round-3 shape G = 8;
+  // profiles/r3zb_k32_tune.txt for R = 1, 2, 4, profiles/r4a_k32_tune.txt for
+  // the rest): R = 1 G16 78.7 % (G8 74.0), R = 2 G16 75.6 (63.9), R = 3 G2
+  // 62.9 (55.0), R = 4 G4 59.6 (54.3), R = 5 G2 53.3 (46.5), R = 6 G2 48.6
+  // (40.4), R = 8 G4 43.2 (36.0); R = 16 keeps G8 (27.8; G4 26.0).
+  static constexpr int G = KM < 8 ? KM : KM == 32 ? g32(RM) : 8;
   static constexpr bool TL = KM >= 8;
   static constexpr bool PAIR = KM == 8 && RM <= 4;  // measured +2.5 % (W2)
 };
@@ -402,6 +409,16 @@ __device__ __forceinline__ void desc_body(const DescArgs &a, cu64 *rec, uint32_t
   cPermTab *gtabs = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
   const DescView v{rec, a.k, a.r};
   auto run = [&](auto tabs0) {
+    if (a.tpw == 1) {  // one tile (desc_tpw's choice unless the grid is huge): no loop
+      const uint32_t base = t0 * TILE;
+      if (base + TILE <= cols)
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs0, a.k, r, cols,
+                                                          base + threadIdx.x);
+      else
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs0, a.k, r, cols,
+                                                         base + threadIdx.x);
+      return;
+    }
     for (uint32_t t = t0; t < t1; t++) {
       // The tables are the same for every tile: without this opaque zero,
       // loop-invariant code motion hoists all k x RM of them out of the tile
@@ -440,6 +457,22 @@ __global__ __launch_bounds__(T) void rs_apply_desc(const DescArgs a) {
   desc_body<KM, RM, T, U, BAR, G, TL, PAIR, COPY>(a, rec, a.r, lds_ptab);
 }
 
+// Shares per load group of the mixed launch's branch with R rows: the table
+// kernel's, except at k = 32, where 16 for every branch measured best in the
+// mixed launch (tools/mixbench.hip on config 6's download shape,
+// profiles/r4b_mixbench32.txt: 74.3 % against 72.8 with the per-R uniform
+// choice and 70.3 with G = 4).
+template <int KM, int R>
+constexpr int mix_g() { return KM == 32 ? 16 : Tune<KM, R>::G; }
+// Inputs two at a time (PAIR: 4.5 instead of 5 VALU per row and dword) in the
+// mixed launch at k = 16 too: 73.1 -> 75.7 % on config 5's download shape,
+// interleaved on one box (profiles/r4c_mixbench16.txt); at k = 32 it lost
+// (75.1 -> 73.1 %). (The uniform k = 16 kernels keep PAIR off: it raised
+// their VGPRs past an occupancy step; the mixed kernel's registers are its
+// largest branch's anyway.)
+template <int KM, int R>
+constexpr bool mix_pair() { return KM == 16 || Tune<KM, R>::PAIR; }
+
 // Mixed row counts in one launch (DescArgs::mix): each workgroup reads its
 // item's count and runs that count's tile (the Tune of that bucket), so a
 // download's chunks -- most lost 1-3 data shares, each a different set --
@@ -457,7 +490,8 @@ __global__ __launch_bounds__(kThreads) void rs_apply_desc_mix(const DescArgs a) 
   {                                                                                         \
     using C = Tune<KM, R>;                                                                  \
     static_assert(C::T == kThreads && C::U == 1, "mixed launch: one tile shape");           \
-    desc_body<KM, R, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR, COPY>(a, rec, r, lds_ptab);  \
+    desc_body<KM, R, C::T, C::U, C::BAR, mix_g<KM, R>(), C::TL, mix_pair<KM, R>(), COPY>(   \
+        a, rec, r, lds_ptab);                                                               \
     return;                                                                                 \
   }
   if (r <= 1) STORB_MIX_CASE(1)

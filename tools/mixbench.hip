@@ -66,7 +66,7 @@ constexpr int gsel(int R) {
   return G;
 }
 
-template <int KM, int R, int G, bool TL, bool INL, int U = 1>
+template <int KM, int R, int G, bool TL, bool INL, int U = 1, bool PAIR = false>
 __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *rec,
                                       PermTab *lds) {
   constexpr uint32_t TILE = kThreads * U;
@@ -78,11 +78,11 @@ __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *
   const uint32_t base = t * TILE;
   auto go = [&](auto tabs) {
     if (base + TILE <= cols)
-      perm_tile<KM, R, kThreads, U, false, G, false, false, false>(v, tabs, a.k, R, cols,
-                                                                 base + threadIdx.x);
-    else
-      perm_tile<KM, R, kThreads, U, false, G, false, true, false>(v, tabs, a.k, R, cols,
+      perm_tile<KM, R, kThreads, U, false, G, PAIR, false, false>(v, tabs, a.k, R, cols,
                                                                 base + threadIdx.x);
+    else
+      perm_tile<KM, R, kThreads, U, false, G, PAIR, true, false>(v, tabs, a.k, R, cols,
+                                                               base + threadIdx.x);
   };
   if constexpr (TL) {
     typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
@@ -96,7 +96,8 @@ __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *
   }
 }
 
-template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0>
+template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0,
+          bool PAIR = false>
 __global__ __launch_bounds__(kThreads) void mixv(const DescArgs a, const Bounds b) {
   __shared__ __attribute__((aligned(16))) PermTab lds[TL ? KM * kMixR : 1];
   const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + kThreads * U - 1) / (kThreads * U);
@@ -107,10 +108,10 @@ __global__ __launch_bounds__(kThreads) void mixv(const DescArgs a, const Bounds 
     r = blockIdx.x >= b.first[4] ? 4 : blockIdx.x >= b.first[3] ? 3 : blockIdx.x >= b.first[2] ? 2 : 1;
   else
     r = static_cast<uint32_t>(rec[0] >> 32);
-  if (r <= 1) return vbody<KM, 1, gsel<KM, G, GSET>(1), TL, INL, U>(a, b, rec, lds);
-  if (r == 2) return vbody<KM, 2, gsel<KM, G, GSET>(2), TL, INL, U>(a, b, rec, lds);
-  if (r == 3) return vbody<KM, 3, gsel<KM, G, GSET>(3), TL, INL, U>(a, b, rec, lds);
-  return vbody<KM, 4, gsel<KM, G, GSET>(4), TL, INL, U>(a, b, rec, lds);
+  if (r <= 1) return vbody<KM, 1, gsel<KM, G, GSET>(1), TL, INL, U, PAIR>(a, b, rec, lds);
+  if (r == 2) return vbody<KM, 2, gsel<KM, G, GSET>(2), TL, INL, U, PAIR>(a, b, rec, lds);
+  if (r == 3) return vbody<KM, 3, gsel<KM, G, GSET>(3), TL, INL, U, PAIR>(a, b, rec, lds);
+  return vbody<KM, 4, gsel<KM, G, GSET>(4), TL, INL, U, PAIR>(a, b, rec, lds);
 }
 
 struct Var {
@@ -121,13 +122,14 @@ struct Var {
   int U = 1;
 };
 
-template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0>
+template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0,
+          bool PAIR = false>
 Var mk(const char *name, int cap) {
   return {name, SORTED, INL, [cap](const DescArgs &a, const Bounds &b, hipStream_t s) {
             const uint64_t tps = ((a.block >> 4) + kThreads * U - 1) / (kThreads * U);
             const size_t dyn = cap_lds(cap, TL ? sizeof(PermTab) * KM * kMixR : 0);
-            return launch_lds<mixv<KM, G, TL, SORTED, INL, U, GSET>>(tps * a.nitems, kThreads, dyn,
-                                                                     s, a, b);
+            return launch_lds<mixv<KM, G, TL, SORTED, INL, U, GSET, PAIR>>(tps * a.nitems, kThreads,
+                                                                           dyn, s, a, b);
           }, {}, U};
 }
 
@@ -139,23 +141,14 @@ std::vector<Var> variants() {
                {}});
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
-  v.push_back(mk<KM, GP, true, false, false>("same shape cap2", 2));
-  v.push_back(mk<KM, GP, true, false, false>("same shape cap3", 3));
-  v.push_back(mk<KM, GP, true, true, true>("sorted TL inline", 0));
-  v.push_back(mk<KM, GP, true, true, true>("sorted TL inline cap2", 2));
-  v.push_back(mk<KM, GP, true, true, true>("sorted TL inline cap3", 3));
-  v.push_back(mk<KM, GP, false, true, true>("sorted noTL inline cap2", 2));
-  v.push_back(mk<KM, GP, false, true, true>("sorted noTL inline cap3", 3));
-  v.push_back(mk<KM, 4, true, false, false, 2>("U2 G4 (TL, rec[0])", 0));
   v.push_back(mk<KM, 4, true, false, false, 2>("U2 G4 cap2", 2));
-  v.push_back(mk<KM, 4, true, false, false, 2>("U2 G4 cap3", 3));
-  v.push_back(mk<KM, 4, true, true, true, 2>("U2 G4 sorted TL inline cap2", 2));
-  v.push_back(mk<KM, GP, true, false, false, 1, 1>("GSET1 (TL, rec[0])", 0));
+  v.push_back(mk<KM, 16, true, false, false>("G16 (TL, rec[0])", 0));
+  v.push_back(mk<KM, 16, true, false, false>("G16 cap3", 3));
+  v.push_back(mk<KM, 16, true, false, false>("G16 cap4", 4));
   v.push_back(mk<KM, GP, true, false, false, 1, 2>("GSET2 (TL, rec[0])", 0));
-  if constexpr (KM == 32) {
-    v.push_back(mk<KM, 16, true, false, false>("G16 (TL, rec[0])", 0));
-    v.push_back(mk<KM, 16, true, false, false>("G16 cap3", 3));
-  }
+  v.push_back(mk<KM, 8, true, false, false, 1, 0, true>("G8 PAIR", 0));
+  v.push_back(mk<KM, 16, true, false, false, 1, 0, true>("G16 PAIR", 0));
+  v.push_back(mk<KM, 8, false, false, false>("G8 noTL", 0));
   return v;
 }
 
