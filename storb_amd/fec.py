@@ -43,11 +43,10 @@ class Fec:
         buf = bytes(data)
         if not buf:
             raise FecError("empty input")
-        parity, B, pad = _lib.thread_context().encode(self.k, self.m, buf)
-        padded = buf + bytes(B * self.k - len(buf))
-        chunks = [Chunk(padded[i * B:(i + 1) * B], i) for i in range(self.k)]
-        chunks += [Chunk(p, self.k + i) for i, p in enumerate(parity)]
-        return chunks, pad
+        # storb_rs_encode_shares, as the Rust shim's Fec::encode: every share
+        # (data shares zero-padded, then parity) written by one call
+        shares, B, pad = _lib.thread_context().encode_shares(self.k, self.m, buf)
+        return [Chunk(s.tobytes(), i) for i, s in enumerate(shares)], pad
 
     def decode(self, chunks: Sequence[Chunk], padlen: int) -> bytes:
         if len(chunks) < self.k:

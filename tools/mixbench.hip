@@ -162,6 +162,110 @@ __global__ void fill(uint64_t *q, uint64_t n, uint64_t seed) {
   }
 }
 
+template <int KM, int R>
+int isolate(int reps, const std::vector<uint32_t> &es, uint32_t N, uint32_t k, uint32_t n,
+            size_t B, uint8_t *d, uint8_t *p, uint8_t *o, size_t ob, hipStream_t s, hipEvent_t e0,
+            hipEvent_t e1, std::mt19937 &rng, double &t_uni_sum, double &t_mix_sum) {
+  uint32_t M = 0;
+  for (uint32_t s2 = 0; s2 < N; s2++) M += es[s2] == R;
+  if (!M) return 0;
+  std::vector<PermTab> tabs(k * R);
+  for (auto &t : tabs) t = perm_tab(uint8_t(rng() | 1));
+  PermTab *dtab;
+  CK(hipMalloc(&dtab, tabs.size() * sizeof(PermTab)));
+  CK(hipMemcpy(dtab, tabs.data(), tabs.size() * sizeof(PermTab), hipMemcpyHostToDevice));
+  // the uniform launch needs equally spaced stripes: the first M stripes
+  auto slot_id = [&](uint32_t c) { return c < R ? k + c : c; };  // slots 0..R-1 <- parity
+  std::vector<uint64_t> rec;
+  for (uint32_t q = 0; q < M; q++) {
+    rec.push_back(0 | (uint64_t(R) << 32));
+    for (uint32_t c = 0; c < k; c++) {
+      const uint32_t id = slot_id(c);
+      rec.push_back(reinterpret_cast<uint64_t>(id < k ? d + q * k * B + id * B
+                                                      : p + q * (n - k) * B + (id - k) * B));
+    }
+    for (uint32_t i = 0; i < kMixR; i++)
+      rec.push_back(i < R ? reinterpret_cast<uint64_t>(o + (size_t(q) * kMixR + i) * B) : 0);
+  }
+  uint64_t *drec;
+  CK(hipMalloc(&drec, rec.size() * 8));
+  CK(hipMemcpy(drec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice));
+  DescArgs da{};
+  da.desc = drec;
+  da.ptab = dtab;
+  da.block = B;
+  da.k = k;
+  da.r = kMixR;
+  da.tpw = 1;
+  da.nitems = M;
+  da.rec_qwords = 1 + k + kMixR;
+  da.mix = 1;
+  ApplyArgs aa{};
+  for (uint32_t c = 0; c < k; c++) {
+    const uint32_t id = slot_id(c);
+    aa.in[c] = id < k ? d + id * B : p + (id - k) * B;
+    aa.in_stride[c] = id < k ? k * B : (n - k) * B;
+  }
+  for (uint32_t i = 0; i < R; i++) {
+    aa.out[i] = o + i * B;
+    aa.out_stride[i] = kMixR * B;
+  }
+  aa.ptab = dtab;
+  aa.k = k;
+  aa.r = R;
+  aa.tab_rows = R;
+  aa.block = B;
+  aa.nstripes = M;
+  using C2 = Tune<KM, R>;
+  auto uni = [&](int cap) {
+    return launch_perm<KM, R, C2::T, C2::U, C2::BAR, C2::G, C2::TL, C2::PAIR>(aa, s, cap);
+  };
+  struct Iso {
+    const char *name;
+    std::function<hipError_t()> fn;
+    std::vector<float> ms;
+  };
+  std::vector<Iso> iso = {
+      {"mixed-row kernel (records)", [&] { return launch_apply_desc(da, s); }, {}},
+      {"uniform rs_apply_perm, tuned cap", [&] { return uni(C2::OCC); }, {}},
+      {"uniform rs_apply_perm, uncapped", [&] { return uni(0); }, {}},
+  };
+  std::vector<uint8_t> w2(ob), g2(ob);
+  for (size_t vi = 0; vi < iso.size(); vi++) {
+    CK(hipMemsetAsync(o, 0xEE, ob, s));
+    CK(iso[vi].fn());
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(vi ? g2.data() : w2.data(), o, ob, hipMemcpyDeviceToHost));
+    if (vi && std::memcmp(w2.data(), g2.data(), ob) != 0) {
+      std::printf("isolation R=%d %s: MISMATCH\n", R, iso[vi].name);
+      return 1;
+    }
+  }
+  for (int r = 0; r < reps; r++)
+    for (auto &v : iso) {
+      CK(hipEventRecord(e0, s));
+      CK(v.fn());
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float x = 0;
+      CK(hipEventElapsedTime(&x, e0, e1));
+      v.ms.push_back(x);
+    }
+  const double b2 = double(M) * (k + R) * B;
+  for (size_t vi = 0; vi < iso.size(); vi++) {
+    auto &v = iso[vi];
+    std::sort(v.ms.begin(), v.ms.end());
+    const float m = v.ms[v.ms.size() / 2];
+    if (vi == 0) t_mix_sum += m;
+    if (vi == 2) t_uni_sum += m;
+    std::printf("k=%u R=%d subset (%u stripes): %-34s %8.4f ms  %6.2f TB/s  %5.1f %%  (bit-exact)\n",
+                k, R, M, v.name, m, b2 / (m * 1e-3) / 1e12, 100.0 * b2 / (m * 1e-3) / 8e12);
+  }
+  CK(hipFree(drec));
+  CK(hipFree(dtab));
+  return 0;
+}
+
 template <int KM>
 int run(int reps) {
   const bool c6 = KM == 32;
@@ -308,106 +412,22 @@ int run(int reps) {
     std::printf("k=%u %-34s %8.4f ms  %6.2f TB/s  %5.1f %%  (bit-exact)\n", k, v.name.c_str(), m,
                 bytes / (m * 1e-3) / 1e12, 100.0 * bytes / (m * 1e-3) / 8e12);
   }
-  // Isolation: only the chunks that lost 2 data shares, every one with the
-  // same survivor slots (lost data shares {0, 1}): the mixed-row kernel over
-  // them (records) against the uniform table kernel over the same stripes
-  // (pointers in kernel arguments), same tables.
-  {
-    std::vector<uint32_t> st2;
-    for (uint32_t s2 = 0; s2 < N; s2++)
-      if (es[s2] == 2) st2.push_back(s2);
-    std::vector<PermTab> tabs(k * 2);
-    for (auto &t : tabs) t = perm_tab(uint8_t(rng() | 1));
-    PermTab *dtab;
-    CK(hipMalloc(&dtab, tabs.size() * sizeof(PermTab)));
-    CK(hipMemcpy(dtab, tabs.data(), tabs.size() * sizeof(PermTab), hipMemcpyHostToDevice));
-    const uint32_t M = static_cast<uint32_t>(st2.size());
-    // the uniform launch needs equally spaced stripes: use the first M stripes
-    std::vector<uint64_t> rec;
-    for (uint32_t q = 0; q < M; q++) {
-      rec.push_back(0 | (uint64_t(2) << 32));
-      for (uint32_t c = 0; c < k; c++) {
-        const uint32_t id = c < 2 ? k + c : c;  // slots 0, 1 <- parity 0, 1
-        rec.push_back(reinterpret_cast<uint64_t>(id < k ? d + q * k * B + id * B
-                                                        : p + q * (n - k) * B + (id - k) * B));
-      }
-      for (uint32_t i = 0; i < kMixR; i++)
-        rec.push_back(i < 2 ? reinterpret_cast<uint64_t>(o + (size_t(q) * kMixR + i) * B) : 0);
-    }
-    uint64_t *drec;
-    CK(hipMalloc(&drec, rec.size() * 8));
-    CK(hipMemcpy(drec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice));
-    DescArgs da{};
-    da.desc = drec;
-    da.ptab = dtab;
-    da.block = B;
-    da.k = k;
-    da.r = kMixR;
-    da.tpw = 1;
-    da.nitems = M;
-    da.rec_qwords = 1 + k + kMixR;
-    da.mix = 1;
-    ApplyArgs aa{};
-    for (uint32_t c = 0; c < k; c++) {
-      const uint32_t id = c < 2 ? k + c : c;
-      aa.in[c] = id < k ? d + id * B : p + (id - k) * B;
-      aa.in_stride[c] = id < k ? k * B : (n - k) * B;
-    }
-    for (uint32_t i = 0; i < 2; i++) {
-      aa.out[i] = o + i * B;
-      aa.out_stride[i] = kMixR * B;
-    }
-    aa.ptab = dtab;
-    aa.k = k;
-    aa.r = 2;
-    aa.tab_rows = 2;
-    aa.block = B;
-    aa.nstripes = M;
-    using C2 = Tune<KM, 2>;
-    auto uni = [&](int cap) {
-      return launch_perm<KM, 2, C2::T, C2::U, C2::BAR, C2::G, C2::TL, C2::PAIR>(aa, s, cap);
-    };
-    struct Iso {
-      const char *name;
-      std::function<hipError_t()> fn;
-      std::vector<float> ms;
-    };
-    std::vector<Iso> iso = {
-        {"r=2 subset: mixed-row kernel (records)", [&] { return launch_apply_desc(da, s); }, {}},
-        {"r=2 subset: uniform rs_apply_perm, tuned cap", [&] { return uni(C2::OCC); }, {}},
-        {"r=2 subset: uniform rs_apply_perm, uncapped", [&] { return uni(0); }, {}},
-    };
-    std::vector<uint8_t> w2(ob), g2(ob);
-    for (size_t vi = 0; vi < iso.size(); vi++) {
-      CK(hipMemsetAsync(o, 0xEE, ob, s));
-      CK(iso[vi].fn());
-      CK(hipStreamSynchronize(s));
-      CK(hipMemcpy(vi ? g2.data() : w2.data(), o, ob, hipMemcpyDeviceToHost));
-      if (vi && std::memcmp(w2.data(), g2.data(), ob) != 0) {
-        std::printf("isolation %s: MISMATCH\n", iso[vi].name);
-        return 1;
-      }
-    }
-    for (int r = 0; r < reps; r++)
-      for (auto &v : iso) {
-        CK(hipEventRecord(e0, s));
-        CK(v.fn());
-        CK(hipEventRecord(e1, s));
-        CK(hipEventSynchronize(e1));
-        float x = 0;
-        CK(hipEventElapsedTime(&x, e0, e1));
-        v.ms.push_back(x);
-      }
-    const double b2 = double(M) * (k + 2) * B;
-    for (auto &v : iso) {
-      std::sort(v.ms.begin(), v.ms.end());
-      const float m = v.ms[v.ms.size() / 2];
-      std::printf("k=%u %-44s %8.4f ms  %6.2f TB/s  %5.1f %%  (bit-exact, %u stripes)\n", k,
-                  v.name, m, b2 / (m * 1e-3) / 1e12, 100.0 * b2 / (m * 1e-3) / 8e12, M);
-    }
-    CK(hipFree(drec));
-    CK(hipFree(dtab));
-  }
+  // Isolation per row count R: the chunks that lost R data shares, each
+  // with the same survivor slots (data shares 0..R-1 lost, rebuilt from the
+  // first R parity shares): the mixed-row kernel over them (records) against
+  // the uniform table kernel over the same stripes (pointers in kernel
+  // arguments), same tables. The three uniform launches back to back against
+  // the one mixed launch over all chunks: how much of the gap to the uniform
+  // 2-lost figure is the mix of row counts rather than the descriptors.
+  double t_uni_sum = 0, t_mix_sum = 0;
+  if (isolate<KM, 1>(reps, es, N, k, n, B, d, p, o, ob, s, e0, e1, rng, t_uni_sum, t_mix_sum) ||
+      isolate<KM, 2>(reps, es, N, k, n, B, d, p, o, ob, s, e0, e1, rng, t_uni_sum, t_mix_sum) ||
+      isolate<KM, 3>(reps, es, N, k, n, B, d, p, o, ob, s, e0, e1, rng, t_uni_sum, t_mix_sum))
+    return 1;
+  std::printf("k=%u all row counts: sum of the uniform launches (uncapped) %.4f ms = %.1f %%, "
+              "sum of the per-count mixed launches %.4f ms = %.1f %%\n", k, t_uni_sum,
+              100.0 * bytes / (t_uni_sum * 1e-3) / 8e12, t_mix_sum,
+              100.0 * bytes / (t_mix_sum * 1e-3) / 8e12);
   CK(hipStreamDestroy(s));
   for (auto &u : ups) {
     CK(hipFree(u.rec));
