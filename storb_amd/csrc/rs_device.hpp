@@ -597,7 +597,9 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
 // k = 16 download mix (tools/descbench.cpp, profiles/r3j_descbench.txt):
 // capped at 2 or 3 per CU 61.5 %, at 4 72.1 %, uncapped 72.4 % of 8 TB/s.
 // k <= 4 keeps the RS(4,2) table kernel's measured cap of 4.
-constexpr int mix_occ(int KM) { return KM <= 4 ? Tune<4, 2>::OCC : 0; }
+// k = 32 (16 shares per group): 3 per CU, +0.5-0.7 % over uncapped in three
+// interleaved runs (profiles/r4{b,c,d}_mixbench32.txt "G16 cap3").
+constexpr int mix_occ(int KM) { return KM <= 4 ? Tune<4, 2>::OCC : KM == 32 ? 3 : 0; }
 
 template <int KM>
 hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
