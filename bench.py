@@ -187,6 +187,12 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
                 "thread_cpu_over_wall": round((r["user_s"] + r["sys_s"]) / el, 3),
                 "minor_faults": r["minflt"], "major_faults": r["majflt"],
                 "minor_faults_per_call": round(r["minflt"] / max(1, r["calls"]), 2),
+                # the thread's own cycles / instructions (perf_event_open; null
+                # where refused): effective clock and IPC over the sample, and
+                # a dependent multiply-add chain's rate before / after it
+                "effective_ghz": round(r["cycles"] / el / 1e9, 3) if r["cycles"] > 0 else None,
+                "ipc": round(r["instructions"] / r["cycles"], 3) if r["cycles"] > 0 else None,
+                "clock_probe_giter_per_s": [round(r["probe_before"], 3), round(r["probe_after"], 3)],
                 "voluntary_switches": r["nvcsw"], "involuntary_switches": r["nivcsw"],
                 **_cpu_where(r["cpu_start"]),
                 # time the hypervisor ran something else on this vCPU: the

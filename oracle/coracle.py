@@ -137,7 +137,9 @@ class BenchStats(C.Structure):
     _fields_ = [("wall_s", C.c_double), ("user_s", C.c_double), ("sys_s", C.c_double),
                 ("minflt", C.c_long), ("majflt", C.c_long), ("nvcsw", C.c_long),
                 ("nivcsw", C.c_long), ("calls", C.c_ulonglong), ("cpu_start", C.c_int),
-                ("cpu_end", C.c_int), ("bad", C.c_int)]
+                ("cpu_end", C.c_int), ("bad", C.c_int), ("cycles", C.c_longlong),
+                ("instructions", C.c_longlong), ("probe_before", C.c_double),
+                ("probe_after", C.c_double)]
 
 
 def bench_roundtrip(k: int, n: int, chunks: np.ndarray, chunk_len: int, nsample: int,

@@ -16,11 +16,15 @@
  *            B bytes, the decode output, the oracle's own scratch) and frees
  *            it: the reported baseline.
  * fresh = 0: every buffer allocated once: the arithmetic alone. */
+#include <linux/perf_event.h>
 #include <sched.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/ioctl.h>
 #include <sys/resource.h>
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "zfec_oracle.h"
 
@@ -31,6 +35,43 @@ static double now_s(void) {
 }
 
 static double tv_s(struct timeval t) { return t.tv_sec + t.tv_usec * 1e-6; }
+
+/* A hardware counter of the calling thread, user mode only; -1 if refused
+ * (containers often forbid perf_event_open). */
+static int perf_open(unsigned long long config) {
+  struct perf_event_attr a;
+  memset(&a, 0, sizeof(a));
+  a.type = PERF_TYPE_HARDWARE;
+  a.size = sizeof(a);
+  a.config = config;
+  a.disabled = 1;
+  a.exclude_kernel = 1;
+  a.exclude_hv = 1;
+  return (int)syscall(__NR_perf_event_open, &a, 0, -1, -1, 0);
+}
+
+static long long perf_read(int fd) {
+  long long v = -1;
+  if (fd < 0 || read(fd, &v, sizeof(v)) != (ssize_t)sizeof(v)) return -1;
+  return v;
+}
+
+/* Clock probe: a dependent multiply-add chain for ~0.1 s; iterations per ns
+ * scale with the core's clock and with nothing else it shares. */
+static double clock_probe(void) {
+  volatile unsigned long long sink;
+  unsigned long long x = 1, it = 0;
+  const double t0 = now_s();
+  double t = t0;
+  while (t - t0 < 0.1) {
+    for (int i = 0; i < 100000; i++) x = x * 6364136223846793005ull + 1442695040888963407ull;
+    it += 100000;
+    t = now_s();
+  }
+  sink = x;
+  (void)sink;
+  return it / ((t - t0) * 1e9);
+}
 
 int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len,
                        unsigned nsample, const unsigned *surv, unsigned nsets, int do_encode,
@@ -55,6 +96,11 @@ int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len
   memset(out_keep, 0, len);
   memset(scratch, 0, (size_t)k * B);
   memset(row, 0, B);
+  out->probe_before = clock_probe();
+  const int fcyc = perf_open(PERF_COUNT_HW_CPU_CYCLES);
+  const int fins = perf_open(PERF_COUNT_HW_INSTRUCTIONS);
+  if (fcyc >= 0) ioctl(fcyc, PERF_EVENT_IOC_ENABLE, 0);
+  if (fins >= 0) ioctl(fins, PERF_EVENT_IOC_ENABLE, 0);
   struct rusage r0, r1;
   getrusage(RUSAGE_THREAD, &r0);
   out->cpu_start = sched_getcpu();
@@ -88,6 +134,11 @@ int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len
   out->wall_s = now_s() - t0;
   out->cpu_end = sched_getcpu();
   getrusage(RUSAGE_THREAD, &r1);
+  out->cycles = perf_read(fcyc);
+  out->instructions = perf_read(fins);
+  if (fcyc >= 0) close(fcyc);
+  if (fins >= 0) close(fins);
+  out->probe_after = clock_probe();
   out->user_s = tv_s(r1.ru_utime) - tv_s(r0.ru_utime);
   out->sys_s = tv_s(r1.ru_stime) - tv_s(r0.ru_stime);
   out->minflt = r1.ru_minflt - r0.ru_minflt;

@@ -85,6 +85,11 @@ typedef struct {
   unsigned long long calls;
   int cpu_start, cpu_end;
   int bad;
+  /* the thread's own hardware counters over the loop (perf_event_open, user
+   * mode; -1 when the kernel refuses them) and a clock probe before / after:
+   * a dependent 64-bit multiply-add chain, iterations per ns */
+  long long cycles, instructions;
+  double probe_before, probe_after;
 } zo_bench_t;
 int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len,
                        unsigned nsample, const unsigned *surv, unsigned nsets, int do_encode,

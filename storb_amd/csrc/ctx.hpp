@@ -129,6 +129,14 @@ struct Pattern {
 };
 
 constexpr int kDescRing = 4;   // page-locked descriptor upload buffers per context
+// Flags of the events recorded after every launch only to ORDER later work
+// (a table's last use before its free, a descriptor slot's last use before
+// it is rewritten): no system-scope release. A default event's record
+// writes back the L2s' dirty lines (up to 4 MiB per XCD of freshly streamed
+// shares) before the next kernel on the stream may start; between the
+// default bench's encode and decode launches that was most of a ~3.5 us
+// boundary.
+constexpr unsigned kOrderEvent = hipEventDisableTiming | hipEventDisableSystemFence;
 constexpr uint64_t kThreadsTable = 256;  // lanes (16-B columns) per table-kernel tile
 
 struct DeviceGuard {

@@ -143,7 +143,7 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
   // launches of its previous use have completed.
   const unsigned slot = ctx->desc_next++ % kDescRing;
   if (ctx->desc_ev[slot]) HIP_TRY(ctx, hipEventSynchronize(ctx->desc_ev[slot]));
-  else HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_ev[slot], hipEventDisableTiming));
+  else HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_ev[slot], kOrderEvent));
   HIP_TRY(ctx, ctx->desc_pin[slot].ensure(total));
   HIP_TRY(ctx, ctx->desc_dev[slot].ensure(total));
   uint8_t *h = ctx->desc_pin[slot].p;

@@ -202,7 +202,8 @@ class Jit {
     for (auto &u : e.uses)
       if (u.device == device && u.stream == s) return hipEventRecord(u.done, s);
     Entry::Use u{device, s, nullptr};
-    hipError_t r = hipEventCreateWithFlags(&u.done, hipEventDisableTiming);
+    // ordering only (the module is unloaded after it): no system-scope fence
+    hipError_t r = hipEventCreateWithFlags(&u.done, hipEventDisableTiming | hipEventDisableSystemFence);
     if (r != hipSuccess) return r;
     e.uses.push_back(u);
     return hipEventRecord(u.done, s);

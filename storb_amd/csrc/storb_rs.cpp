@@ -129,7 +129,7 @@ int tables_used(storb_rs_ctx *ctx, Tables *t, hipStream_t s) {
       return STORB_RS_OK;
     }
   hipEvent_t e = nullptr;
-  HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventCreateWithFlags(&e, kOrderEvent));
   t->uses.emplace_back(s, e);
   HIP_TRY(ctx, hipEventRecord(e, s));
   return STORB_RS_OK;

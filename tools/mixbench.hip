@@ -96,8 +96,13 @@ __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *
   }
 }
 
+// Paired inputs per branch: PSET 0 none, 1 all, 2 R <= 3, 3 R <= 2.
+constexpr bool psel(int PSET, int R) {
+  return PSET == 1 || (PSET == 2 && R <= 3) || (PSET == 3 && R <= 2);
+}
+
 template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0,
-          bool PAIR = false>
+          int PSET = 0>
 __global__ __launch_bounds__(kThreads) void mixv(const DescArgs a, const Bounds b) {
   __shared__ __attribute__((aligned(16))) PermTab lds[TL ? KM * kMixR : 1];
   const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + kThreads * U - 1) / (kThreads * U);
@@ -108,10 +113,10 @@ __global__ __launch_bounds__(kThreads) void mixv(const DescArgs a, const Bounds 
     r = blockIdx.x >= b.first[4] ? 4 : blockIdx.x >= b.first[3] ? 3 : blockIdx.x >= b.first[2] ? 2 : 1;
   else
     r = static_cast<uint32_t>(rec[0] >> 32);
-  if (r <= 1) return vbody<KM, 1, gsel<KM, G, GSET>(1), TL, INL, U, PAIR>(a, b, rec, lds);
-  if (r == 2) return vbody<KM, 2, gsel<KM, G, GSET>(2), TL, INL, U, PAIR>(a, b, rec, lds);
-  if (r == 3) return vbody<KM, 3, gsel<KM, G, GSET>(3), TL, INL, U, PAIR>(a, b, rec, lds);
-  return vbody<KM, 4, gsel<KM, G, GSET>(4), TL, INL, U, PAIR>(a, b, rec, lds);
+  if (r <= 1) return vbody<KM, 1, gsel<KM, G, GSET>(1), TL, INL, U, psel(PSET, 1)>(a, b, rec, lds);
+  if (r == 2) return vbody<KM, 2, gsel<KM, G, GSET>(2), TL, INL, U, psel(PSET, 2)>(a, b, rec, lds);
+  if (r == 3) return vbody<KM, 3, gsel<KM, G, GSET>(3), TL, INL, U, psel(PSET, 3)>(a, b, rec, lds);
+  return vbody<KM, 4, gsel<KM, G, GSET>(4), TL, INL, U, psel(PSET, 4)>(a, b, rec, lds);
 }
 
 struct Var {
@@ -123,12 +128,12 @@ struct Var {
 };
 
 template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0,
-          bool PAIR = false>
+          int PSET = 0>
 Var mk(const char *name, int cap) {
   return {name, SORTED, INL, [cap](const DescArgs &a, const Bounds &b, hipStream_t s) {
             const uint64_t tps = ((a.block >> 4) + kThreads * U - 1) / (kThreads * U);
             const size_t dyn = cap_lds(cap, TL ? sizeof(PermTab) * KM * kMixR : 0);
-            return launch_lds<mixv<KM, G, TL, SORTED, INL, U, GSET, PAIR>>(tps * a.nitems, kThreads,
+            return launch_lds<mixv<KM, G, TL, SORTED, INL, U, GSET, PSET>>(tps * a.nitems, kThreads,
                                                                            dyn, s, a, b);
           }, {}, U};
 }
@@ -141,14 +146,18 @@ std::vector<Var> variants() {
                {}});
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
-  v.push_back(mk<KM, 4, true, false, false, 2>("U2 G4 cap2", 2));
-  v.push_back(mk<KM, 16, true, false, false>("G16 (TL, rec[0])", 0));
-  v.push_back(mk<KM, 16, true, false, false>("G16 cap3", 3));
-  v.push_back(mk<KM, 16, true, false, false>("G16 cap4", 4));
-  v.push_back(mk<KM, GP, true, false, false, 1, 2>("GSET2 (TL, rec[0])", 0));
-  v.push_back(mk<KM, 8, true, false, false, 1, 0, true>("G8 PAIR", 0));
-  v.push_back(mk<KM, 16, true, false, false, 1, 0, true>("G16 PAIR", 0));
-  v.push_back(mk<KM, 8, false, false, false>("G8 noTL", 0));
+  if constexpr (KM == 16) {
+    v.push_back(mk<KM, 8, true, false, false, 1, 0, 1>("G8 PAIR all", 0));
+    v.push_back(mk<KM, 8, true, false, false, 1, 0, 2>("G8 PAIR R<=3", 0));
+    v.push_back(mk<KM, 8, true, false, false, 1, 0, 3>("G8 PAIR R<=2", 0));
+    v.push_back(mk<KM, 4, true, false, false, 1, 0, 1>("G4 PAIR all", 0));
+    v.push_back(mk<KM, 4, true, false, false, 1, 0, 2>("G4 PAIR R<=3", 0));
+    v.push_back(mk<KM, 8, true, false, false, 1, 1, 1>("GSET1 PAIR all", 0));
+  } else {
+    v.push_back(mk<KM, 16, true, false, false>("G16 (TL, rec[0])", 0));
+    v.push_back(mk<KM, 16, true, false, false>("G16 cap3", 3));
+    v.push_back(mk<KM, 16, true, false, false, 1, 0, 3>("G16 cap3 PAIR R<=2", 3));
+  }
   return v;
 }
 
