@@ -193,6 +193,11 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
                 "effective_ghz": round(r["cycles"] / el / 1e9, 3) if r["cycles"] > 0 else None,
                 "ipc": round(r["instructions"] / r["cycles"], 3) if r["cycles"] > 0 else None,
                 "clock_probe_giter_per_s": [round(r["probe_before"], 3), round(r["probe_after"], 3)],
+                # after the sample, this thread: the oracle's addmul on an
+                # L1-resident block, sequential reads from L2 and from DRAM
+                "l1_addmul_GBps": round(r["l1_addmul_gbs"], 2),
+                "l2_read_GBps": round(r["l2_read_gbs"], 2),
+                "dram_read_GBps": round(r["dram_read_gbs"], 2),
                 "voluntary_switches": r["nvcsw"], "involuntary_switches": r["nivcsw"],
                 **_cpu_where(r["cpu_start"]),
                 # time the hypervisor ran something else on this vCPU: the

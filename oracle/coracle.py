@@ -139,7 +139,8 @@ class BenchStats(C.Structure):
                 ("nivcsw", C.c_long), ("calls", C.c_ulonglong), ("cpu_start", C.c_int),
                 ("cpu_end", C.c_int), ("bad", C.c_int), ("cycles", C.c_longlong),
                 ("instructions", C.c_longlong), ("probe_before", C.c_double),
-                ("probe_after", C.c_double)]
+                ("probe_after", C.c_double), ("l1_addmul_gbs", C.c_double),
+                ("l2_read_gbs", C.c_double), ("dram_read_gbs", C.c_double)]
 
 
 def bench_roundtrip(k: int, n: int, chunks: np.ndarray, chunk_len: int, nsample: int,

@@ -73,6 +73,51 @@ static double clock_probe(void) {
   return it / ((t - t0) * 1e9);
 }
 
+/* Sequential read of `bytes` by this thread, GB/s (best of 3 passes). */
+static double read_probe(size_t bytes) {
+  uint64_t *b = malloc(bytes);
+  if (!b) return -1;
+  const size_t n = bytes / 8;
+  for (size_t i = 0; i < n; i++) b[i] = i * 0x9E3779B97F4A7C15ull;
+  volatile uint64_t sink;
+  double best = 0;
+  for (int pass = 0; pass < 3; pass++) {
+    uint64_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+    const int reps = bytes <= (1u << 20) ? 200 : 1;
+    const double t0 = now_s();
+    for (int r = 0; r < reps; r++)
+      for (size_t i = 0; i + 4 <= n; i += 4) {
+        acc0 += b[i];
+        acc1 += b[i + 1];
+        acc2 += b[i + 2];
+        acc3 += b[i + 3];
+      }
+    const double el = now_s() - t0;
+    sink = acc0 ^ acc1 ^ acc2 ^ acc3;
+    const double gbs = (double)bytes * reps / el / 1e9;
+    if (gbs > best) best = gbs;
+  }
+  (void)sink;
+  free(b);
+  return best;
+}
+
+/* The oracle's own addmul over an L1-resident 4 KiB block, GB/s of src. */
+static double l1_addmul_probe(void) {
+  static uint8_t src[4096], dst[4096];
+  for (int i = 0; i < 4096; i++) src[i] = (uint8_t)(i * 31 + 7);
+  zo_addmul(dst, src, 0x53, sizeof(src));
+  const double t0 = now_s();
+  int it = 0;
+  double t = t0;
+  while (t - t0 < 0.05) {
+    for (int r = 0; r < 256; r++) zo_addmul(dst, src, (uint8_t)(0x53 + r), sizeof(src));
+    it += 256;
+    t = now_s();
+  }
+  return (double)it * sizeof(src) / (t - t0) / 1e9;
+}
+
 int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len,
                        unsigned nsample, const unsigned *surv, unsigned nsets, int do_encode,
                        int do_decode, int fresh, double seconds, zo_bench_t *out) {
@@ -139,6 +184,9 @@ int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len
   if (fcyc >= 0) close(fcyc);
   if (fins >= 0) close(fins);
   out->probe_after = clock_probe();
+  out->l1_addmul_gbs = l1_addmul_probe();
+  out->l2_read_gbs = read_probe(512u << 10);
+  out->dram_read_gbs = read_probe(256u << 20);
   out->user_s = tv_s(r1.ru_utime) - tv_s(r0.ru_utime);
   out->sys_s = tv_s(r1.ru_stime) - tv_s(r0.ru_stime);
   out->minflt = r1.ru_minflt - r0.ru_minflt;

@@ -202,6 +202,11 @@ int zo_fec_new(unsigned k, unsigned n, uint8_t *enc) {
 /* ------------------------------------------------------------- encode */
 #define ZO_STRIDE 8192 /* fec.c STRIDE blocking of the addmul loop */
 
+void zo_addmul(uint8_t *dst, const uint8_t *src, uint8_t c, size_t sz) {
+  zo_init();
+  addmul(dst, src, c, sz);
+}
+
 /* scratch (k*B bytes) / enc (n*k): caller-provided buffers for the
  * allocation-free CPU baseline (cpu_bench.c); NULL = allocate per call, as
  * zfec-rs does (a Fec per chunk, piece.rs:328; Vecs per share). */

@@ -90,7 +90,13 @@ typedef struct {
    * a dependent 64-bit multiply-add chain, iterations per ns */
   long long cycles, instructions;
   double probe_before, probe_after;
+  /* memory-side probes after the loop, GB/s: the oracle's addmul on an
+   * L1-resident 4 KiB block, a 512 KiB (L2) and a 256 MiB (DRAM) sequential
+   * read by this thread */
+  double l1_addmul_gbs, l2_read_gbs, dram_read_gbs;
 } zo_bench_t;
+/* fec.c's addmul (dst ^= c * src) as the oracle runs it (cpu_bench.c probe) */
+void zo_addmul(uint8_t *dst, const uint8_t *src, uint8_t c, size_t sz);
 int zo_bench_roundtrip(unsigned k, unsigned n, const uint8_t *chunks, size_t len,
                        unsigned nsample, const unsigned *surv, unsigned nsets, int do_encode,
                        int do_decode, int fresh, double seconds, zo_bench_t *out);

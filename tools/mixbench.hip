@@ -121,10 +121,11 @@ __global__ __launch_bounds__(kThreads) void mixv(const DescArgs a, const Bounds 
 
 struct Var {
   std::string name;
-  bool sorted, inl;
+  bool sorted, inl;  // sorted: ascending row count, r from the launch arguments
   std::function<hipError_t(const DescArgs &, const Bounds &, hipStream_t)> fn;
   std::vector<float> ms;
   int U = 1;
+  bool heavy_first = false;  // records ordered by descending row count (r still from rec[0])
 };
 
 template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0,
@@ -144,6 +145,13 @@ std::vector<Var> variants() {
   v.push_back({"product rs_apply_desc_mix", false, false,
                [](const DescArgs &a, const Bounds &, hipStream_t s) { return launch_apply_desc(a, s); },
                {}});
+  {
+    Var h{"product kernel, heaviest items first", false, false,
+          [](const DescArgs &a, const Bounds &, hipStream_t s) { return launch_apply_desc(a, s); },
+          {}};
+    h.heavy_first = true;
+    v.push_back(h);
+  }
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
   if constexpr (KM == 16) {
@@ -325,13 +333,15 @@ int run(int reps) {
   const uint32_t tps = static_cast<uint32_t>((B / 16 + kThreads - 1) / kThreads);
   const uint32_t tab_q = 1 + k + kMixR;
   const uint32_t rec_plain = 1 + k + kMixR, rec_inl = tab_q + 4 * k * kMixR;
-  auto build = [&](bool sorted, bool inl, int U, std::vector<uint64_t> &rec,
+  auto build = [&](bool sorted, bool inl, int U, bool heavy_first, std::vector<uint64_t> &rec,
                    std::vector<PermTab> &tab, Bounds &b) {
     const uint32_t tpsU = static_cast<uint32_t>((B / 16 + kThreads * U - 1) / (kThreads * U));
     std::vector<uint32_t> ord(items.size());
     for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
     if (sorted)
       std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return items[x].e < items[y].e; });
+    if (heavy_first)
+      std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return items[x].e > items[y].e; });
     rec.clear();
     tab.clear();
     b = Bounds{};
@@ -368,7 +378,7 @@ int run(int reps) {
   for (size_t vi = 0; vi < vs.size(); vi++) {
     std::vector<uint64_t> rec;
     std::vector<PermTab> tab;
-    build(vs[vi].sorted, vs[vi].inl, vs[vi].U, rec, tab, ups[vi].b);
+    build(vs[vi].sorted, vs[vi].inl, vs[vi].U, vs[vi].heavy_first, rec, tab, ups[vi].b);
     CK(hipMalloc(&ups[vi].rec, rec.size() * 8));
     CK(hipMemcpy(ups[vi].rec, rec.data(), rec.size() * 8, hipMemcpyHostToDevice));
     CK(hipMalloc(&ups[vi].tab, std::max<size_t>(1, tab.size()) * sizeof(PermTab)));
