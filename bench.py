@@ -535,9 +535,66 @@ def shard_hash_rate(ctx, w, stream, reps=3):
     e1.synchronize()
     ms = e0.elapsed_time(e1) / reps
     nbytes = w.N * w.n * w.B
-    return {"value": round(nbytes / (ms * 1e-3) / 1e9, 1), "unit": "GB/s of shard bytes",
-            "ms": round(ms, 4), "shards": w.N * w.n, "shard_bytes": w.B,
-            "what": "blake3 (Storb piece id) of all data+parity shards, batched kernel"}
+    res = {"value": round(nbytes / (ms * 1e-3) / 1e9, 1), "unit": "GB/s of shard bytes",
+           "ms": round(ms, 4), "shards": w.N * w.n, "shard_bytes": w.B,
+           "what": "blake3 (Storb piece id) of all data+parity shards, batched kernel"}
+    res["encode_with_piece_ids"] = encode_hashed_rate(ctx, w, stream, hd, hp)
+    return res
+
+
+def encode_hashed_rate(ctx, w, stream, hd, hp, reps=5):
+    """Encode plus every share's piece id (upload.rs:418-420 then :623), device
+    resident, two ways: the encode kernel then the hash kernel over the shards
+    it left in HBM (k*B read twice, parity written then read back), and
+    storb_rs_encode_hashed_dev, which for (2, 3) / (4, 6) runs one kernel that
+    hashes each share while it encodes (rs_encode_hash<k, n-k>, every byte
+    crosses HBM once). Self-checked: both give the same parity and digests.
+    Both are VALU-bound (blake3's compression), so the fused figure is
+    reported against the two-kernel one, with the HBM bytes it moves."""
+    k, n, B, N = w.k, w.n, w.B, w.N
+    sp = stream.cuda_stream
+    dev = w.data.device
+    h = torch.empty(N * n * 32, dtype=torch.uint8, device=dev)
+
+    def two():
+        ctx.encode_batch_dev(k, n, B, N, w.dptr, w.pptr, stream=sp)
+        ctx.blake3_batch_dev(w.dptr, B, N * k, B, hd.data_ptr(), stream=sp)
+        ctx.blake3_batch_dev(w.pptr, B, N * (n - k), B, hp.data_ptr(), stream=sp)
+
+    def fused():
+        ctx.encode_hashed_dev(k, n, B, N, w.dptr, w.pptr, h.data_ptr(), stream=sp)
+
+    two()
+    par_ref = w.parity.clone()
+    with torch.cuda.stream(stream):
+        w.parity.zero_()
+    fused()
+    stream.synchronize()
+    want = torch.cat([hd.view(N, k, 32), hp.view(N, n - k, 32)], dim=1).reshape(-1)
+    ok = torch.equal(w.parity, par_ref) and torch.equal(h, want)
+    del par_ref
+    if not ok:
+        raise SystemExit("encode_hashed_dev mismatch against encode + blake3")
+    res = {"what": "device-resident encode + blake3 of all n shares per stripe",
+           "self_check": "parity and digests equal between the two paths"}
+    for name, go in (("two_kernels", two), ("one_call", fused)):
+        go()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            go()
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        res[name] = {"ms": round(ms, 4),
+                     "GiBps_user": round(N * w.chunk / GIB / (ms * 1e-3), 1)}
+    fused_kernel = (k, n) in ((2, 3), (4, 6)) and B % 1024 == 0 and B <= (256 << 10)
+    res["one_call"]["kernel"] = (f"rs_encode_hash<{k},{n - k}>" if fused_kernel
+                                 else "encode kernel + blake3_batch_kernel")
+    res["one_call"]["hbm_GBps_algorithmic"] = round(
+        N * n * B / (res["one_call"]["ms"] * 1e-3) / 1e9, 1)
+    res["speedup"] = round(res["two_kernels"]["ms"] / res["one_call"]["ms"], 3)
+    return res
 
 
 def download_sets(k, n, nchunks, seed, fail=0.0):

@@ -257,6 +257,19 @@ int storb_rs_blake3_batch_dev(storb_rs_ctx *ctx, const uint8_t *d_in, size_t len
                               uint32_t count, size_t stride, uint8_t *d_out,
                               void *hip_stream);
 
+/* Encode with the piece ids (upload.rs:623 hashes every piece
+ * right after encode_chunk): layout as storb_rs_encode_batch_dev, and the
+ * blake3 digest of share t of stripe s (t < k data, then parity) at
+ * d_hashes + (s*n + t)*32. (k, n) = (2, 3) / (4, 6) with block a multiple of
+ * 1 KiB up to 256 KiB and 16-B aligned pointers run one kernel that hashes
+ * every share while it encodes (each byte crosses HBM once); other
+ * geometries run the encode kernel, then the hash kernel. */
+int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
+                               size_t block, uint32_t nstripes,
+                               const uint8_t *d_data, size_t data_stride,
+                               uint8_t *d_parity, size_t parity_stride,
+                               uint8_t *d_hashes, void *hip_stream);
+
 /* ---- synthetic input (benchmarks / tests) ----------------------------- */
 /* Object o (o < nobj) at d + o*obj_stride gets obj_len bytes of the
  * little-endian splitmix64 stream seeded with seed_base + o. */

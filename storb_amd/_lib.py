@@ -118,6 +118,8 @@ def _declare(L):
     L.storb_blake3.argtypes = [vp, sz, vp]
     L.storb_blake3.restype = None
     L.storb_rs_blake3_batch_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, vp, vp]
+    L.storb_rs_encode_hashed_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
+                                             vp, sz, vp, sz, vp, vp]
     L.storb_rs_decode_chunks.argtypes = [vp, C.c_uint32, C.c_uint32, sz, sz, C.c_uint32,
                                          C.POINTER(vp), C.POINTER(C.c_uint32),
                                          C.POINTER(C.c_uint32), vp, sz]
@@ -605,6 +607,16 @@ class Context:
         rc = lib().storb_rs_blake3_batch_dev(self._h, d_in, length, count, stride, d_out,
                                              self._s(stream))
         self._check(rc, "storb_rs_blake3_batch_dev")
+
+    def encode_hashed_dev(self, k: int, n: int, block: int, nstripes: int, d_data: int,
+                          d_parity: int, d_hashes: int, data_stride: int = 0,
+                          parity_stride: int = 0, stream: Optional[int] = None):
+        """Encode plus the blake3 piece id of every share: digest of share t of
+        stripe s at d_hashes + (s*n + t)*32 (storb_rs_encode_hashed_dev)."""
+        rc = lib().storb_rs_encode_hashed_dev(self._h, k, n, block, nstripes, d_data,
+                                              data_stride, d_parity, parity_stride, d_hashes,
+                                              self._s(stream))
+        self._check(rc, "storb_rs_encode_hashed_dev")
 
     def set_kernel(self, variant: int):
         self._check(lib().storb_rs_set_kernel(self._h, variant), "storb_rs_set_kernel")

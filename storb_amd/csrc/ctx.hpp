@@ -179,6 +179,9 @@ struct storb_rs_ctx {
   // storb_rs_encode_chunks without piece ids: zero-copy kernels (1) or
   // SDMA H2D -> kernel -> D2H (0). STORB_RS_ZC_BATCH.
   bool zc_batch = true;
+  // Encode + blake3 piece ids in one kernel (rs_encode_hash.hip) where the
+  // geometry has one; 0 = encode kernel then hash kernel. STORB_RS_FUSED_HASH.
+  bool fused_hash = true;
   hipEvent_t slice_ev[storb_rs::detail::kMaxSlices] = {};  // sliced single-call pipeline
   // Slice-completion words the single-call streams write (64 B apart) and
   // the host spins on (host_calls.cpp slice_signal / slice_wait).
@@ -272,6 +275,14 @@ int apply(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
 int encode_apply(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *const *d_in,
                  const size_t *in_stride, uint8_t *const *d_out, const size_t *out_stride,
                  size_t block, uint32_t nstripes, hipStream_t s);
+// Encode + blake3 of all n shares in one kernel (rs_encode_hash.hip), digest
+// of share t of stripe s at d_hashes + (s*n + t)*32: true if launched (*err
+// its launch status), false if the geometry / alignment has no fused kernel
+// or ctx->fused_hash is off.
+bool try_encode_hash(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                     uint32_t nstripes, const uint8_t *d_data, size_t data_stride,
+                     uint8_t *d_parity, size_t parity_stride, uint8_t *d_hashes, hipStream_t s,
+                     hipError_t *err);
 // decode_chunk's selection (first k by index) and zfec's slot arrangement.
 int select_shares(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint32_t *share_idx,
                   uint32_t nshares, std::vector<uint32_t> &slot_idx,

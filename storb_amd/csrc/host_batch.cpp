@@ -61,6 +61,10 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
       HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
   }
   const uint32_t nb = (nchunks + batch - 1) / batch;
+  // Piece ids from the encode kernel itself (rs_encode_hash.hip) where the
+  // geometry has one: digests land in [c][n] order.
+  const bool fused = hashes_out && p > 0 && ctx->fused_hash && S == B &&
+                     encode_hash_supported(k, n, B);
   HostPool &pool = host_pool(ctx);
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;
@@ -77,7 +81,11 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
         });
       }
     }
-    if (hashes_out) {
+    if (hashes_out && fused) {
+      std::memcpy(hashes_out + static_cast<size_t>(c0) * n * 32,
+                  ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch,
+                  static_cast<size_t>(cn) * n * 32);
+    } else if (hashes_out) {
       // device order: [c][j] data digests, then [c][i] parity digests
       const uint8_t *hd = ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch;
       const uint8_t *hp = hd + static_cast<size_t>(cn) * k * 32;
@@ -138,7 +146,11 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     uint8_t *dp = dd + per * batch;
     uint8_t *dh = dp + static_cast<size_t>(p) * S * batch;  // digests (if any)
     HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
-    if (p > 0) {
+    hipError_t fe = hipSuccess;
+    if (fused && try_encode_hash(ctx, k, n, B, cn, dd, per, dp, static_cast<size_t>(p) * S, dh,
+                                 s, &fe)) {
+      HIP_TRY(ctx, fe);
+    } else if (p > 0) {
       std::vector<const uint8_t *> in(k);
       std::vector<uint8_t *> out(p);
       std::vector<size_t> ins(k, per), outs(p, static_cast<size_t>(p) * S);
@@ -149,7 +161,7 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
       if (rc) return rc;
     }
     size_t back = static_cast<size_t>(p) * S * cn;
-    if (hashes_out) {
+    if (hashes_out && !fused) {
       // shares are pitched S apart across the whole batch: one launch each
       HIP_TRY(ctx, launch_blake3_batch(dd, B, cn * k, S, dh, s));
       if (p > 0)

@@ -99,6 +99,26 @@ hipError_t launch_encode_bitslice_stream(const ApplyArgs &a, uint32_t n, const S
 hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
                                uint64_t stride, uint8_t *out, hipStream_t s);
 
+// Encode with the blake3 digest of every share in the same pass
+// (rs_encode_hash.hip). Stripe s: data share j at data + s*data_stride +
+// j*block, parity share i at parity + s*parity_stride + i*block, digest of
+// share t (data then parity) at hashes + (s*n + t)*32. 16-B aligned.
+constexpr int kEHMaxTabs = 8;
+struct EncHashArgs {
+  const uint8_t *data;
+  uint64_t data_stride;
+  uint8_t *parity;
+  uint64_t parity_stride;
+  uint8_t *hashes;
+  uint64_t block;
+  uint32_t nstripes, nchunks, seg_log2, pad;
+  uint32_t tab[kEHMaxTabs][5];  // [j*(n-k) + i]: perm_tab(parity coefficient)
+};
+// (k, n) in {(2, 3), (4, 6)} -- Storb's geometries for chunks up to 1 MiB --
+// and block a multiple of 1 KiB up to 256 KiB.
+bool encode_hash_supported(uint32_t k, uint32_t n, uint64_t block);
+hipError_t launch_encode_hash(const EncHashArgs &a, uint32_t k, uint32_t n, hipStream_t s);
+
 // The streamed single-call kernel (rs_stream.hip): k <= 32, 1 <= r <= 8,
 // one stripe, dwordx4-aligned slots; hipErrorInvalidValue otherwise.
 hipError_t launch_apply_stream(const ApplyArgs &a, const StreamArgs &st, hipStream_t s);

@@ -519,6 +519,7 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   c->zc_max = 64ull << 20;
   if (const char *e = std::getenv("STORB_RS_ZC_MAX")) c->zc_max = std::strtoull(e, nullptr, 10);
   if (const char *e = std::getenv("STORB_RS_ZC_BATCH")) c->zc_batch = std::atoi(e) != 0;
+  if (const char *e = std::getenv("STORB_RS_FUSED_HASH")) c->fused_hash = std::atoi(e) != 0;
   if (const char *e = std::getenv("STORB_RS_TABLE_CACHE"))
     c->table_cap = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
   if (const char *e = std::getenv("STORB_RS_TEST_STREAM_STALL")) {
@@ -889,6 +890,107 @@ int storb_rs_blake3_batch_dev(storb_rs_ctx *ctx, const uint8_t *d_in, size_t len
   DeviceGuard g(ctx->device);
   HIP_TRY(ctx, launch_blake3_batch(d_in, len, count, stride, d_out,
                                    pick_stream(ctx, hip_stream)));
+  return STORB_RS_OK;
+}
+
+}  // extern "C"
+
+namespace storb_rs {
+namespace detail {
+
+// The one-kernel encode + piece ids when the geometry has one and the
+// pointers are dwordx4-aligned (false: nothing launched).
+bool try_encode_hash(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                     uint32_t nstripes, const uint8_t *d_data, size_t data_stride,
+                     uint8_t *d_parity, size_t parity_stride, uint8_t *d_hashes, hipStream_t s,
+                     hipError_t *err) {
+  *err = hipSuccess;
+  if (!ctx->fused_hash || !encode_hash_supported(k, n, block)) return false;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(d_data) | reinterpret_cast<uintptr_t>(d_parity) |
+                       reinterpret_cast<uintptr_t>(d_hashes) | data_stride | parity_stride;
+  if (al & 15) return false;
+  const uint32_t p = n - k;
+  const std::vector<uint8_t> &enc = cached_enc(k, n);
+  EncHashArgs a{};
+  a.data = d_data;
+  a.data_stride = data_stride;
+  a.parity = d_parity;
+  a.parity_stride = parity_stride;
+  a.hashes = d_hashes;
+  a.block = block;
+  a.nstripes = nstripes;
+  a.nchunks = static_cast<uint32_t>(block / 1024);
+  while ((1u << a.seg_log2) < a.nchunks) a.seg_log2++;
+  for (uint32_t j = 0; j < k; j++)
+    for (uint32_t i = 0; i < p; i++) {
+      const PermTab t = perm_tab(enc[static_cast<size_t>(k + i) * k + j]);
+      uint32_t *w = a.tab[j * p + i];
+      w[0] = t.t0lo;
+      w[1] = t.t0hi;
+      w[2] = t.t1lo;
+      w[3] = t.t1hi;
+      w[4] = t.t2;
+    }
+  *err = launch_encode_hash(a, k, n, s);
+  return true;
+}
+
+}  // namespace detail
+}  // namespace storb_rs
+
+extern "C" {
+
+int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                               uint32_t nstripes, const uint8_t *d_data, size_t data_stride,
+                               uint8_t *d_parity, size_t parity_stride, uint8_t *d_hashes,
+                               void *hip_stream) {
+  if (!ctx) return STORB_RS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!valid_params(k, n)) return fail(ctx, STORB_RS_EINVAL, "invalid (k, n)");
+  if (block == 0 || nstripes == 0) return STORB_RS_OK;
+  if (!d_data || !d_hashes || (n > k && !d_parity))
+    return fail(ctx, STORB_RS_EINVAL, "null device pointer");
+  if (block > 16ull * 1024 * 1024)
+    return fail(ctx, STORB_RS_EINVAL, "blake3: share larger than 16 MiB");
+  if (data_stride == 0) data_stride = static_cast<size_t>(k) * block;
+  if (parity_stride == 0) parity_stride = static_cast<size_t>(n - k) * block;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = pick_stream(ctx, hip_stream);
+  hipError_t e;
+  if (n > k && try_encode_hash(ctx, k, n, block, nstripes, d_data, data_stride, d_parity,
+                               parity_stride, d_hashes, s, &e)) {
+    HIP_TRY(ctx, e);
+    return STORB_RS_OK;
+  }
+  // Two kernels: encode, then one hash launch per share slot into a
+  // stream-ordered scratch, scattered to (s*n + t)*32.
+  const uint32_t p = n - k;
+  if (p > 0) {
+    std::vector<const uint8_t *> in(k);
+    std::vector<size_t> ins(k, data_stride), outs(p, parity_stride);
+    std::vector<uint8_t *> out(p);
+    for (uint32_t j = 0; j < k; j++) in[j] = d_data + static_cast<size_t>(j) * block;
+    for (uint32_t i = 0; i < p; i++) out[i] = d_parity + static_cast<size_t>(i) * block;
+    const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), block,
+                                nstripes, s);
+    if (rc) return rc;
+  }
+  uint8_t *tmp = nullptr;
+  const size_t per = static_cast<size_t>(nstripes) * 32;
+  HIP_TRY(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), per * n, s));
+  hipError_t err = hipSuccess;
+  for (uint32_t t = 0; t < n && err == hipSuccess; t++) {
+    const uint8_t *base = t < k ? d_data + static_cast<size_t>(t) * block
+                                : d_parity + static_cast<size_t>(t - k) * block;
+    err = launch_blake3_batch(base, block, nstripes, t < k ? data_stride : parity_stride,
+                              tmp + t * per, s);
+    if (err == hipSuccess)
+      err = hipMemcpy2DAsync(d_hashes + static_cast<size_t>(t) * 32, static_cast<size_t>(n) * 32,
+                             tmp + t * per, 32, 32, nstripes, hipMemcpyDeviceToDevice, s);
+  }
+  const hipError_t ef = hipFreeAsync(tmp, s);
+  HIP_TRY(ctx, err);
+  HIP_TRY(ctx, ef);
   return STORB_RS_OK;
 }
 

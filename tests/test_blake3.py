@@ -133,6 +133,89 @@ def test_device_hashes_of_encoded_shards(ctx):
             assert got.tobytes() == want, (s, i)
 
 
+def _hashed_case(ctx, k, n, B, N, seed, data_stride=0, parity_stride=0, check_all=True):
+    """storb_rs_encode_hashed_dev on N stripes of splitmix data: parity against
+    the oracle's encode, every digest against the host blake3 of that share."""
+    import torch
+    from oracle import coracle
+    ds = data_stride or k * B
+    ps = parity_stride or (n - k) * B
+    data = torch.zeros(N * ds, dtype=torch.uint8, device="cuda:0")
+    par = torch.full((N * ps,), 0xA5, dtype=torch.uint8, device="cuda:0")
+    hashes = torch.full((N * n * 32,), 0x5A, dtype=torch.uint8, device="cuda:0")
+    ctx.fill_splitmix_dev(data.data_ptr(), k * B, N, ds, seed)
+    ctx.encode_hashed_dev(k, n, B, N, data.data_ptr(), par.data_ptr(), hashes.data_ptr(),
+                          data_stride, parity_stride)
+    torch.cuda.synchronize()
+    par = par.cpu().numpy()
+    got = hashes.cpu().numpy().reshape(N, n, 32)
+    stripes = range(N) if check_all else sorted({0, 1, N // 2, N - 1})
+    for s in stripes:
+        shares, _, _ = coracle.encode(k, n, coracle.splitmix_bytes(seed + s, k * B))
+        for i in range(k, n):
+            o = s * ps + (i - k) * B
+            assert np.array_equal(par[o:o + B], shares[i]), (k, n, B, s, i)
+        for t in range(n):
+            assert got[s, t].tobytes() == _lib.blake3(shares[t].tobytes()), (k, n, B, s, t)
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n,B,N", [
+    (4, 6, 256 << 10, 6),   # Storb's 1 MiB chunk: 256 chunks per share, one stripe per workgroup
+    (4, 6, 128 << 10, 5),   # 512 KiB chunks (config 1): two stripes per workgroup, one dead
+    (2, 3, 128 << 10, 7),   # the storb-faithful 256 KiB chunk of config 4
+    (4, 6, 1 << 10, 300),   # one chunk per share: the chunk is the root
+    (4, 6, 3 << 10, 100),   # 3 chunks: the odd node carried up
+    (2, 3, 5 << 10, 77),    # 5 chunks, 51 stripes per workgroup
+    (4, 6, 255 << 10, 3),   # 255 chunks
+    (4, 6, 2 << 10, 1)])
+def test_encode_hashed_dev_fused_kernel(ctx, k, n, B, N):
+    _hashed_case(ctx, k, n, B, N, 0x5709B + B + N, check_all=N * B <= (8 << 20))
+
+
+@pytest.mark.gpu
+def test_encode_hashed_dev_strided_and_unfused_geometries(ctx):
+    # pitched stripes (fused kernel); geometries without a fused kernel run
+    # encode then hash and scatter the digests into the same layout
+    _hashed_case(ctx, 4, 6, 64 << 10, 9, 11, data_stride=(4 << 16) + 4096,
+                 parity_stride=(2 << 16) + 512)
+    _hashed_case(ctx, 16, 24, 32 << 10, 5, 12)
+    _hashed_case(ctx, 4, 6, 1000, 4, 13)          # not a multiple of 1 KiB
+    _hashed_case(ctx, 4, 6, 512 << 10, 2, 14)     # over 256 KiB per share
+    _hashed_case(ctx, 3, 5, 4 << 10, 3, 15)
+
+
+@pytest.mark.gpu
+def test_encode_hashed_dev_fused_equals_two_kernel_path(monkeypatch):
+    """STORB_RS_FUSED_HASH=0 (encode kernel, then hash kernel) and the fused
+    kernel give the same parity and digests, and the batch entry point
+    (storb_rs_encode_chunks_hashed) returns them too."""
+    import torch
+    k, n, B, N = 4, 6, 256 << 10, 12
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("STORB_RS_FUSED_HASH", fused)
+        c = _lib.Context(0)
+        try:
+            data = torch.empty(N * k * B, dtype=torch.uint8, device="cuda:0")
+            par = torch.empty(N * (n - k) * B, dtype=torch.uint8, device="cuda:0")
+            h = torch.empty(N * n * 32, dtype=torch.uint8, device="cuda:0")
+            c.fill_splitmix_dev(data.data_ptr(), k * B, N, k * B, 99)
+            c.encode_hashed_dev(k, n, B, N, data.data_ptr(), par.data_ptr(), h.data_ptr())
+            torch.cuda.synchronize()
+            host = data.cpu().numpy()
+            p2, h2 = c.encode_chunks_hashed(k, n, host, k * B, N)
+            outs.append((par.cpu().numpy(), h.cpu().numpy(), np.asarray(p2).ravel(),
+                         np.asarray(h2).ravel()))
+        finally:
+            c.close()
+    (pa, ha, pb, hb), (qa, ga, qb, gb) = outs
+    assert np.array_equal(pa, qa) and np.array_equal(ha, ga)
+    assert np.array_equal(pa, pb) and np.array_equal(ha, hb)
+    assert np.array_equal(qa, qb) and np.array_equal(ga, gb)
+
+
 @pytest.mark.gpu
 def test_device_batch_rejects_oversize(ctx):
     with pytest.raises(_lib.StorbRsError) as e:
