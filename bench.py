@@ -505,12 +505,67 @@ def shim_path_rate(ctx, seconds=0.4):
             row[name] = {"median_us": round(us, 2), "p10_us": round(lat[len(lat) // 10] / 1e3, 2),
                          "GiBps": round(chunk / GIB / (us * 1e-6), 3), "calls": len(lat),
                          "thread_cpu_over_wall": round((time.thread_time() - c0) / wall, 3)}
+        if (k, n) == (4, 6):
+            row["numa"] = _shim_numa(ctx, {"encode_call": enc_call, "decode_call": dec_call},
+                                     chunk, seconds)
         rows.append(row)
     res["geometries"] = rows
     # Not measured here: the box's SDMA PCIe ceiling in user bytes of RS(4,2)
     # encode (57 GB/s both directions / 1.5 bytes per user byte), cited from
     # tools/pcie_probe.py's run, profiles/r1_pcie_probe.jsonl.
     res["cited_sdma_ceiling_GiBps_user"] = {"value": 35.5, "source": "profiles/r1_pcie_probe.jsonl"}
+    return res
+
+
+def _node_cpus():
+    """{numa node: [allowed logical CPUs]} for this process's affinity set."""
+    out = {}
+    for c in sorted(os.sched_getaffinity(0)):
+        node = _cpu_where(c)["numa_node"]
+        out.setdefault(node, []).append(c)
+    return out
+
+
+def _shim_numa(ctx, calls, chunk, seconds):
+    """The same single calls with the calling thread pinned to the CPUs of the
+    GPU's NUMA node, then to those of another node of the allowed set: a
+    pageable call's host copies cross the socket link when the caller sits on
+    the other node (storb_rs_device_numa_node says which is which)."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    gnode = _lib.lib().storb_rs_device_numa_node(ctx.device)
+    by_node = _node_cpus()
+    res = {"gpu_numa_node": gnode,
+           "allowed_cpus_per_node": {str(k): len(v) for k, v in by_node.items()},
+           "caller_cpu_during_default_run": _cpu_where(libc.sched_getcpu())}
+    if gnode < 0 or gnode not in by_node:
+        res["skipped"] = "GPU node unknown or not in the allowed CPU set"
+        return res
+    others = [n for n in by_node if n != gnode and n is not None]
+    saved = os.sched_getaffinity(0)
+    try:
+        for label, node in (("caller_on_gpu_node", gnode),
+                            ("caller_on_other_node", others[0] if others else None)):
+            if node is None:
+                res[label] = None
+                continue
+            os.sched_setaffinity(0, by_node[node])
+            r = {"node": node}
+            for name, f in calls.items():
+                f()
+                lat = []
+                t0 = time.perf_counter()
+                while time.perf_counter() - t0 < seconds or len(lat) < 11:
+                    t = time.perf_counter_ns()
+                    f()
+                    lat.append(time.perf_counter_ns() - t)
+                lat.sort()
+                us = lat[len(lat) // 2] / 1e3
+                r[name] = {"median_us": round(us, 2),
+                           "GiBps": round(chunk / GIB / (us * 1e-6), 3)}
+            res[label] = r
+    finally:
+        os.sched_setaffinity(0, saved)
     return res
 
 

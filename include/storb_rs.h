@@ -57,6 +57,11 @@ const char *storb_rs_version(void);
 const char *storb_rs_strerror(int code);
 /* Number of HIP devices visible (0 when none; never an error). */
 int storb_rs_device_count(void);
+/* NUMA node of the host socket device `device` hangs off (sysfs), -1 if
+ * unknown. A caller's thread on another node pays the socket link on every
+ * pageable single call (host copies into the page-locked staging, which the
+ * runtime places near the device): pin upload / download tasks there. */
+int storb_rs_device_numa_node(int device);
 /* device_ordinal >= 0 pins the context to that GPU; -1 picks devices
  * round-robin across contexts (objects partition across GPUs). */
 int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out);

@@ -118,6 +118,7 @@ def _declare(L):
     L.storb_blake3.argtypes = [vp, sz, vp]
     L.storb_blake3.restype = None
     L.storb_rs_blake3_batch_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, vp, vp]
+    L.storb_rs_device_numa_node.argtypes = [C.c_int]
     L.storb_rs_encode_hashed_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
                                              vp, sz, vp, sz, vp, vp]
     L.storb_rs_decode_chunks.argtypes = [vp, C.c_uint32, C.c_uint32, sz, sz, C.c_uint32,

@@ -53,24 +53,47 @@ struct DevBuf {
   }
 };
 
+// Page-locked memory on NUMA node `node` (mmap + mbind + first touch, then
+// hipHostRegister, mapped for zero-copy kernels); unpin_node frees it.
+hipError_t pin_alloc_node(size_t n, int node, uint8_t **p);
+void pin_free_node(uint8_t *p, size_t n);
+// STORB_RS_STAGING_NODE: node for the staging buffers (-1, the default:
+// where hipHostMalloc puts them).
+int staging_node_env();
+
 struct PinBuf {
   uint8_t *p = nullptr;
   size_t cap = 0;
-  ~PinBuf() {
-    if (p) (void)hipHostFree(p);
-  }
+  int node = -1;  // >= 0: pin_alloc_node memory on that node
+  ~PinBuf() { release(); }
   void release() {
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      if (node >= 0)
+        pin_free_node(p, cap);
+      else
+        (void)hipHostFree(p);
+    }
     p = nullptr;
     cap = 0;
+    node = -1;
   }
-  hipError_t ensure(size_t n) {
-    if (n <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault);
-    if (e == hipSuccess) cap = n;
+  // want: NUMA node for a new allocation (-1: the runtime's choice, -2: the
+  // STORB_RS_STAGING_NODE setting).
+  hipError_t ensure(size_t n, int want = -2) {
+    if (want == -2) want = staging_node_env();
+    if (n <= cap && want == node) return hipSuccess;
+    release();
+    hipError_t e;
+    if (want >= 0) {
+      e = pin_alloc_node(n, want, &p);
+      if (e == hipSuccess) node = want;
+    } else {
+      e = hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault);
+    }
+    if (e == hipSuccess)
+      cap = n;
+    else
+      p = nullptr;
     return e;
   }
 };

@@ -18,7 +18,13 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+#include <cstdio>
 #include <cstring>
+#include <string>
 #include <functional>
 #include <map>
 #include <memory>
@@ -499,6 +505,63 @@ int storb_rs_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+}  // extern "C"
+
+namespace storb_rs {
+namespace detail {
+
+int staging_node_env() {
+  static const int v = [] {
+    const char *e = std::getenv("STORB_RS_STAGING_NODE");
+    return e ? std::atoi(e) : -1;
+  }();
+  return v;
+}
+
+hipError_t pin_alloc_node(size_t n, int node, uint8_t **out) {
+  *out = nullptr;
+  if (node < 0 || node >= 64) return hipErrorInvalidValue;
+  void *m = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (m == MAP_FAILED) return hipErrorOutOfMemory;
+  const unsigned long mask = 1ul << node;
+  // MPOL_BIND (2): pages come from `node` only
+  if (syscall(SYS_mbind, m, n, 2, &mask, sizeof(mask) * 8 + 1, 0) != 0) {
+    munmap(m, n);
+    return hipErrorInvalidValue;
+  }
+  std::memset(m, 0, n);  // first touch places the pages
+  const hipError_t e = hipHostRegister(m, n, hipHostRegisterPortable | hipHostRegisterMapped);
+  if (e != hipSuccess) {
+    munmap(m, n);
+    return e;
+  }
+  *out = static_cast<uint8_t *>(m);
+  return hipSuccess;
+}
+
+void pin_free_node(uint8_t *p, size_t n) {
+  (void)hipHostUnregister(p);
+  munmap(p, n);
+}
+
+}  // namespace detail
+}  // namespace storb_rs
+
+extern "C" {
+
+int storb_rs_device_numa_node(int device) {
+  char bus[32] = {};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+  for (char *c = bus; *c; c++) *c = static_cast<char>(std::tolower(*c));
+  const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+  FILE *f = std::fopen(path.c_str(), "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
 }
 
 int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
