@@ -57,9 +57,11 @@ struct DevBuf {
 // hipHostRegister, mapped for zero-copy kernels); unpin_node frees it.
 hipError_t pin_alloc_node(size_t n, int node, uint8_t **p);
 void pin_free_node(uint8_t *p, size_t n);
-// STORB_RS_STAGING_NODE: node for the staging buffers (-1, the default:
-// where hipHostMalloc puts them).
-int staging_node_env();
+// STORB_RS_STAGING_NODE: unset = the single calls stage on the calling
+// thread's node, -1 = where hipHostMalloc puts the buffers, N = node N.
+int staging_node_env();  // -2 when unset
+// NUMA node of logical CPU `cpu` (sysfs, cached; -1 unknown).
+int cpu_numa_node(int cpu);
 
 struct PinBuf {
   uint8_t *p = nullptr;
@@ -77,10 +79,8 @@ struct PinBuf {
     cap = 0;
     node = -1;
   }
-  // want: NUMA node for a new allocation (-1: the runtime's choice, -2: the
-  // STORB_RS_STAGING_NODE setting).
-  hipError_t ensure(size_t n, int want = -2) {
-    if (want == -2) want = staging_node_env();
+  // want: NUMA node for a new allocation (-1: the runtime's choice).
+  hipError_t ensure(size_t n, int want = -1) {
     if (n <= cap && want == node) return hipSuccess;
     release();
     hipError_t e;
@@ -188,7 +188,18 @@ struct storb_rs_ctx {
   std::string last_error;
   storb_rs::detail::DevBuf stage;
   storb_rs::detail::DevBuf pipe_dev[2];
-  storb_rs::detail::PinBuf pin_in, pin_out;
+  // Page-locked staging of the single calls, one pair per NUMA node of the
+  // calling thread (host_calls.cpp use_caller_staging): the host copies stay
+  // on the caller's socket and the device reaches the buffer over the
+  // fabric -- a caller on the other socket than the GPU went 65.3 -> 59.5
+  // us per (4, 6) 1 MiB encode, one on the GPU's socket is unchanged at
+  // 51.4-51.9 (profiles/r4n_staging_numa.txt). Slot kStagingNodes: placed by the
+  // runtime (STORB_RS_STAGING_NODE=-1, or the node is unknown).
+  static constexpr int kStagingNodes = 8;
+  storb_rs::detail::PinBuf pin_in_node[kStagingNodes + 1], pin_out_node[kStagingNodes + 1];
+  storb_rs::detail::PinBuf *pin_in = &pin_in_node[kStagingNodes];
+  storb_rs::detail::PinBuf *pin_out = &pin_out_node[kStagingNodes];
+  int pin_node = -1;  // NUMA node of *pin_in / *pin_out (-1: runtime placement)
   storb_rs::detail::PinBuf pipe_in[2], pipe_out[2];
   std::map<std::vector<uint8_t>, std::unique_ptr<storb_rs::detail::Tables>> tables;
   size_t table_cap = 1024;  // cached matrices (STORB_RS_TABLE_CACHE), LRU-evicted

@@ -10,6 +10,8 @@
 #include <chrono>
 #include <cstring>
 #include <mutex>
+#include <sched.h>
+
 #include <thread>
 #include <vector>
 
@@ -297,6 +299,19 @@ extern "C" {
 // shares are written too, B bytes each, the last one zero-padded -- what
 // zfec-rs Fec::encode returns beside the parity (piece.rs:329). Those copies
 // run on the host pool while the kernel works on the parity.
+// Staging for this call on the calling thread's NUMA node (ctx.hpp
+// pin_in_node): sched_getcpu is a vDSO read, the buffers are allocated once
+// per node and kept.
+static void use_caller_staging(storb_rs_ctx *ctx) {
+  int node = staging_node_env();
+  if (node == -2) node = cpu_numa_node(sched_getcpu());
+  const int slot = node >= 0 && node < storb_rs_ctx::kStagingNodes ? node
+                                                                  : storb_rs_ctx::kStagingNodes;
+  ctx->pin_in = &ctx->pin_in_node[slot];
+  ctx->pin_out = &ctx->pin_out_node[slot];
+  ctx->pin_node = slot < storb_rs_ctx::kStagingNodes ? node : -1;
+}
+
 static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *data,
                       size_t len, uint8_t *const *parity_out, size_t *block_out,
                       size_t *padlen_out, uint8_t *const *data_out = nullptr) {
@@ -346,8 +361,9 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   for (uint32_t i = 0; out_direct && i < p; i++)
     out_direct = aligned(parity_out[i]) && range_pinned(parity_out[i], B);
   DeviceGuard g(ctx->device);
-  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(p) * S));
+  use_caller_staging(ctx);
+  if (!in_direct) HIP_TRY(ctx, ctx->pin_in->ensure(static_cast<size_t>(k) * S, ctx->pin_node));
+  if (!out_direct) HIP_TRY(ctx, ctx->pin_out->ensure(static_cast<size_t>(p) * S, ctx->pin_node));
   if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(n) * S));
   HostPool &pool = host_pool(ctx);
   hipStream_t s = ctx->stream;
@@ -364,7 +380,7 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       const size_t src = static_cast<size_t>(j) * B + off;
       size_t avail = off < B ? std::min(cnt, B - off) : 0;
       avail = src < len ? std::min(avail, len - src) : 0;
-      uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(j) * S + off;
+      uint8_t *dst = ctx->pin_in->p + static_cast<size_t>(j) * S + off;
       if (avail) segs.push_back({dst, data + src, avail});
       if (cnt > avail) segs.push_back({dst + avail, nullptr, cnt - avail});
     }
@@ -375,17 +391,17 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
     if (!c) return;
     segs.clear();
     for (uint32_t i = 0; i < p; i++)
-      segs.push_back({parity_out[i] + off, ctx->pin_out.p + static_cast<size_t>(i) * S + off, c});
+      segs.push_back({parity_out[i] + off, ctx->pin_out->p + static_cast<size_t>(i) * S + off, c});
     pool.copy_segs(segs.data(), segs.size());
   };
   if (zc) {  // the kernel reads and writes page-locked host memory over PCIe
     uint8_t *dd, *dp = nullptr;
-    HIP_TRY(ctx, host_dev_ptr(in_direct ? const_cast<uint8_t *>(data) : ctx->pin_in.p, &dd));
+    HIP_TRY(ctx, host_dev_ptr(in_direct ? const_cast<uint8_t *>(data) : ctx->pin_in->p, &dd));
     std::vector<uint8_t *> pd(p);
     if (out_direct) {
       for (uint32_t i = 0; i < p; i++) HIP_TRY(ctx, host_dev_ptr(parity_out[i], &pd[i]));
     } else {
-      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dp));
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out->p, &dp));
       for (uint32_t i = 0; i < p; i++) pd[i] = dp + static_cast<size_t>(i) * S;
     }
     auto launch = [&](size_t off, size_t cnt) {
@@ -418,13 +434,13 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   }
   pack(0, S);
   uint8_t *dd = ctx->stage.p, *dp = ctx->stage.p + static_cast<size_t>(k) * S;
-  HIP_TRY(ctx, hipMemcpyAsync(dd, ctx->pin_in.p, static_cast<size_t>(k) * S,
+  HIP_TRY(ctx, hipMemcpyAsync(dd, ctx->pin_in->p, static_cast<size_t>(k) * S,
                               hipMemcpyHostToDevice, s));
   for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * S;
   for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * S;
   int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), S, 1, s);
   if (rc) return rc;
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dp, static_cast<size_t>(p) * S,
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out->p, dp, static_cast<size_t>(p) * S,
                               hipMemcpyDeviceToHost, s));
   put_data();
   HIP_TRY(ctx, hipStreamSynchronize(s));
@@ -476,8 +492,9 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   const bool out_direct = zc && S == block && padlen == 0 && aligned(out) &&
                           range_pinned(out, outlen);
   DeviceGuard g(ctx->device);
-  if (!in_direct) HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  if (!out_direct) HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(e) * S));
+  use_caller_staging(ctx);
+  if (!in_direct) HIP_TRY(ctx, ctx->pin_in->ensure(static_cast<size_t>(k) * S, ctx->pin_node));
+  if (!out_direct) HIP_TRY(ctx, ctx->pin_out->ensure(static_cast<size_t>(e) * S, ctx->pin_node));
   if (!zc) HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + e) * S));
   // columns [off, off + cnt) of row `row` of the chunk (truncated at outlen)
   auto put_cols = [&](uint32_t row, size_t off, size_t cnt, const uint8_t *src) {
@@ -493,7 +510,7 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       const uint8_t *src = shares[slot_pos[c]] + off;
       const size_t avail = off < block ? std::min(cnt, block - off) : 0;
       if (!in_direct) {
-        uint8_t *dst = ctx->pin_in.p + static_cast<size_t>(c) * S + off;
+        uint8_t *dst = ctx->pin_in->p + static_cast<size_t>(c) * S + off;
         if (avail) segs.push_back({dst, src, avail});
         if (cnt > avail) segs.push_back({dst + avail, nullptr, cnt - avail});
       }
@@ -505,7 +522,7 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
     if (out_direct) return;
     segs.clear();
     for (uint32_t r = 0; r < e; r++)
-      put_cols(missing[r], off, cnt, ctx->pin_out.p + static_cast<size_t>(r) * S + off);
+      put_cols(missing[r], off, cnt, ctx->pin_out->p + static_cast<size_t>(r) * S + off);
     pool.copy_segs(segs.data(), segs.size());
   };
   hipStream_t s = ctx->stream;
@@ -519,14 +536,14 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       for (uint32_t c = 0; c < k; c++)
         HIP_TRY(ctx, host_dev_ptr(const_cast<uint8_t *>(shares[slot_pos[c]]), &id[c]));
     } else {
-      HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &base));
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_in->p, &base));
       for (uint32_t c = 0; c < k; c++) id[c] = base + static_cast<size_t>(c) * S;
     }
     if (out_direct) {
       HIP_TRY(ctx, host_dev_ptr(out, &base));
       for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(missing[r]) * block;
     } else {
-      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &base));
+      HIP_TRY(ctx, host_dev_ptr(ctx->pin_out->p, &base));
       for (uint32_t r = 0; r < e; r++) od[r] = base + static_cast<size_t>(r) * S;
     }
     auto launch = [&](size_t off, size_t cnt) {
@@ -551,13 +568,13 @@ static int decode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   }
   pack(0, S);
   uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
-  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+  HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in->p, static_cast<size_t>(k) * S,
                               hipMemcpyHostToDevice, s));
   for (uint32_t c = 0; c < k; c++) in[c] = din + static_cast<size_t>(c) * S;
   for (uint32_t r = 0; r < e; r++) o[r] = dout + static_cast<size_t>(r) * S;
   rc = apply(ctx, k, e, coef.data(), in.data(), ins.data(), o.data(), outs.data(), S, 1, s);
   if (rc) return rc;
-  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(e) * S,
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out->p, dout, static_cast<size_t>(e) * S,
                               hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   unpack(0, S);
@@ -582,21 +599,22 @@ static int repair_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
   }
   const size_t S = round_up(block, kAlign);
   DeviceGuard g(ctx->device);
-  HIP_TRY(ctx, ctx->pin_in.ensure(static_cast<size_t>(k) * S));
-  HIP_TRY(ctx, ctx->pin_out.ensure(static_cast<size_t>(ntargets) * S));
+  use_caller_staging(ctx);
+  HIP_TRY(ctx, ctx->pin_in->ensure(static_cast<size_t>(k) * S, ctx->pin_node));
+  HIP_TRY(ctx, ctx->pin_out->ensure(static_cast<size_t>(ntargets) * S, ctx->pin_node));
   HIP_TRY(ctx, ctx->stage.ensure(static_cast<size_t>(k + ntargets) * S));
   for (uint32_t c = 0; c < k; c++) {
-    std::memcpy(ctx->pin_in.p + static_cast<size_t>(c) * S, shares[slot_pos[c]], block);
-    std::memset(ctx->pin_in.p + static_cast<size_t>(c) * S + block, 0, S - block);
+    std::memcpy(ctx->pin_in->p + static_cast<size_t>(c) * S, shares[slot_pos[c]], block);
+    std::memset(ctx->pin_in->p + static_cast<size_t>(c) * S + block, 0, S - block);
   }
   hipStream_t s = ctx->stream;
   const bool zc = static_cast<size_t>(k + ntargets) * S <= ctx->zc_max;
   uint8_t *din = ctx->stage.p, *dout = ctx->stage.p + static_cast<size_t>(k) * S;
   if (zc) {  // zero-copy: the kernel works on the pinned staging directly
-    HIP_TRY(ctx, host_dev_ptr(ctx->pin_in.p, &din));
-    HIP_TRY(ctx, host_dev_ptr(ctx->pin_out.p, &dout));
+    HIP_TRY(ctx, host_dev_ptr(ctx->pin_in->p, &din));
+    HIP_TRY(ctx, host_dev_ptr(ctx->pin_out->p, &dout));
   } else {
-    HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in.p, static_cast<size_t>(k) * S,
+    HIP_TRY(ctx, hipMemcpyAsync(din, ctx->pin_in->p, static_cast<size_t>(k) * S,
                                 hipMemcpyHostToDevice, s));
   }
   std::vector<const uint8_t *> in(k);
@@ -609,11 +627,11 @@ static int repair_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
              s);
   if (rc) return rc;
   if (!zc)
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out.p, dout, static_cast<size_t>(ntargets) * S,
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pin_out->p, dout, static_cast<size_t>(ntargets) * S,
                                 hipMemcpyDeviceToHost, s));
   HIP_TRY(ctx, hipStreamSynchronize(s));
   for (uint32_t r = 0; r < ntargets; r++)
-    std::memcpy(out[r], ctx->pin_out.p + static_cast<size_t>(r) * S, block);
+    std::memcpy(out[r], ctx->pin_out->p + static_cast<size_t>(r) * S, block);
   return STORB_RS_OK;
 }
 

@@ -515,9 +515,25 @@ namespace detail {
 int staging_node_env() {
   static const int v = [] {
     const char *e = std::getenv("STORB_RS_STAGING_NODE");
-    return e ? std::atoi(e) : -1;
+    return e && *e ? std::max(-1, std::atoi(e)) : -2;
   }();
   return v;
+}
+
+int cpu_numa_node(int cpu) {
+  static const std::vector<int> map = [] {
+    std::vector<int> m;
+    for (int c = 0; c < 4096; c++) {
+      const std::string dir = "/sys/devices/system/cpu/cpu" + std::to_string(c);
+      if (access(dir.c_str(), F_OK) != 0) break;
+      int node = -1;
+      for (int n = 0; n < 64 && node < 0; n++)
+        if (access((dir + "/node" + std::to_string(n)).c_str(), F_OK) == 0) node = n;
+      m.push_back(node);
+    }
+    return m;
+  }();
+  return cpu >= 0 && cpu < static_cast<int>(map.size()) ? map[cpu] : -1;
 }
 
 hipError_t pin_alloc_node(size_t n, int node, uint8_t **out) {
@@ -526,8 +542,9 @@ hipError_t pin_alloc_node(size_t n, int node, uint8_t **out) {
   void *m = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (m == MAP_FAILED) return hipErrorOutOfMemory;
   const unsigned long mask = 1ul << node;
-  // MPOL_BIND (2): pages come from `node` only
-  if (syscall(SYS_mbind, m, n, 2, &mask, sizeof(mask) * 8 + 1, 0) != 0) {
+  // MPOL_PREFERRED (1): pages from `node` while it has free memory, else
+  // from the nearest node that does (BIND would fault on an exhausted node)
+  if (syscall(SYS_mbind, m, n, 1, &mask, sizeof(mask) * 8 + 1, 0) != 0) {
     munmap(m, n);
     return hipErrorInvalidValue;
   }

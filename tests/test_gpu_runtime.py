@@ -197,3 +197,74 @@ def test_encode_shares_all_n_shares_match_oracle(ctx, k, n, L):
     assert (b, p) == (B, pad)
     for i in range(n):
         assert got[i].tobytes() == bytes(want[i]), i
+
+
+def _nodes():
+    """{numa node: [allowed CPUs]} of this process."""
+    out = {}
+    for c in sorted(os.sched_getaffinity(0)):
+        node = -1
+        try:
+            for name in os.listdir(f"/sys/devices/system/cpu/cpu{c}"):
+                if name.startswith("node") and name[4:].isdigit():
+                    node = int(name[4:])
+        except OSError:
+            pass
+        out.setdefault(node, []).append(c)
+    return out
+
+
+def test_single_calls_stage_on_each_callers_node(ctx):
+    """The single calls stage on the calling thread's NUMA node (ctx.hpp
+    pin_in_node): the same context called from a thread pinned to each node
+    of the allowed set -- one pair of staging buffers per node, the kernel
+    reading each over the fabric -- encodes and decodes oracle-exact, for the
+    streamed (4, 6), the wide (16, 24) and the repair path, and the device's
+    node is reported."""
+    assert _lib.lib().storb_rs_device_numa_node(ctx.device) >= -1
+    saved = os.sched_getaffinity(0)
+    try:
+        for node, cpus in _nodes().items():
+            os.sched_setaffinity(0, cpus)
+            for k, n, L in ((4, 6, 1 << 20), (16, 24, 8 << 20), (2, 3, 100001)):
+                data = rnd(L, 70 + k + node)
+                want, B, pad = coracle.encode(k, n, data)
+                got, b, p = ctx.encode(k, n, data)
+                assert (b, p) == (B, pad)
+                for i in range(n - k):
+                    assert got[i] == bytes(want[k + i]), (node, k, i)
+                surv = list(range(n - k, n))  # the last k shares: data lost 0 .. n-k-1
+                out = ctx.decode(k, n, [bytes(want[i]) for i in surv], surv, B, pad)
+                assert out == data.tobytes(), (node, k, surv)
+            sh, B, _ = coracle.encode(4, 6, rnd(1 << 18, 9))
+            rep = ctx.repair(4, 6, [bytes(sh[i]) for i in (1, 2, 3, 4)], [1, 2, 3, 4], B, [0, 5])
+            assert rep == [bytes(sh[0]), bytes(sh[5])], node
+    finally:
+        os.sched_setaffinity(0, saved)
+
+
+def test_staging_node_env_placements():
+    """STORB_RS_STAGING_NODE=-1 (runtime placement, the pre-round-4 staging)
+    and =0 (every call on node 0) in child processes: oracle-exact."""
+    import subprocess
+    import sys
+    code = ("import numpy as np\n"
+            "from oracle import coracle\n"
+            "from storb_amd import _lib\n"
+            "c = _lib.Context(0)\n"
+            "for k, n, L in ((4, 6, 1 << 20), (16, 24, 8 << 20)):\n"
+            "    d = np.frombuffer(np.random.default_rng(L).bytes(L), dtype=np.uint8).copy()\n"
+            "    want, B, pad = coracle.encode(k, n, d)\n"
+            "    got, b, p = c.encode(k, n, d)\n"
+            "    assert all(got[i] == bytes(want[k + i]) for i in range(n - k))\n"
+            "    surv = list(range(n - k, n))\n"
+            "    assert c.decode(k, n, [bytes(want[i]) for i in surv[:k]], surv[:k], B, pad) == d.tobytes()\n"
+            "c.close()\n"
+            "print('staging ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for v in ("-1", "0"):
+        env = dict(os.environ, STORB_RS_STAGING_NODE=v)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                           timeout=240, env=env, cwd=root)
+        assert r.returncode == 0 and "staging ok" in r.stdout, (v, r.stdout[-2000:],
+                                                               r.stderr[-3000:])
