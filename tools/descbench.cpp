@@ -16,7 +16,8 @@
 // build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/descbench.cpp -Iinclude \
 //   -Istorb_amd/csrc -Lstorb_amd/lib -lstorb_rs -Wl,-rpath,'$ORIGIN/../../storb_amd/lib' \
 //   -o tools/_build/descbench
-// usage: descbench [REPS] [K]; K = 32 runs config 6's download shape instead
+// usage: descbench [REPS] [K]; K = 4 runs the default line's download leg (config
+// 2's geometry); K = 32 runs config 6's download shape instead
 // (32 chunks x 32 MiB, k = 32, n = 48, B = 1 MiB; 4 / 14 / 13 / 1 chunks lost
 // 0 / 1 / 2 / 3 data shares, the histogram of profiles/r3k_bench_c6_download.json).
 #include <hip/hip_runtime.h>
@@ -44,10 +45,14 @@ using namespace storb_rs;
 
 int main(int argc, char **argv) {
   const int reps = argc > 1 ? std::atoi(argv[1]) : 20;
-  const bool c6 = argc > 2 && std::atoi(argv[2]) == 32;
-  const uint32_t k = c6 ? 32 : 16, n = k + k / 2, N = c6 ? 32 : 128;
-  const size_t B = c6 ? (1u << 20) : (512u << 10);
-  const int hist[4] = {c6 ? 4 : 13, c6 ? 14 : 48, c6 ? 13 : 58, c6 ? 1 : 9};
+  const int karg = argc > 2 ? std::atoi(argv[2]) : 16;
+  const bool c6 = karg == 32, c2 = karg == 4;
+  const uint32_t k = c6 ? 32 : c2 ? 4 : 16, n = k + k / 2, N = c6 ? 32 : c2 ? 1024 : 128;
+  const size_t B = c6 ? (1u << 20) : c2 ? (256u << 10) : (512u << 10);
+  // K = 4: the default bench line's download leg (1024 x 1 MiB chunks, 349 /
+  // 675 lost 0 / 1 data shares, BENCH download_decode histogram)
+  const int hist[4] = {c6 ? 4 : c2 ? 349 : 13, c6 ? 14 : c2 ? 675 : 48, c6 ? 13 : c2 ? 0 : 58,
+                       c6 ? 1 : c2 ? 0 : 9};
   uint8_t *d = nullptr, *p = nullptr;
   CK(hipMalloc(&d, N * k * B));
   CK(hipMalloc(&p, N * (n - k) * B));
@@ -195,7 +200,7 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(dmrec, mrec.data(), mrec.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dmtab, mtab.data(), mtab.size() * sizeof(PermTab), hipMemcpyHostToDevice));
   for (uint32_t cap : {0u, 2u, 3u, 4u, 6u, 8u}) {
-    for (uint32_t tpw : {1u, 2u}) {
+    for (uint32_t tpw : {1u, 2u, 4u}) {
       DescArgs a{};
       a.desc = dmrec;
       a.ptab = dmtab;
@@ -227,15 +232,19 @@ int main(int argc, char **argv) {
     std::printf("product call host time (returns before the kernels end): median %.1f us\n",
                 hus[hus.size() / 2]);
   }
-  // uniform reference: 2 lost everywhere, table kernel
+  // uniform reference: 2 lost everywhere (K = 4: 1 lost, as the download),
+  // table kernel
   storb_rs_set_kernel(ctx, STORB_RS_KERNEL_PERM);
+  const uint32_t ul = c2 ? 1 : 2;
   std::vector<uint32_t> s2;
-  for (uint32_t i = 2; i < n && s2.size() < k; i++) s2.push_back(i);
+  for (uint32_t i = ul; i < n && s2.size() < k; i++) s2.push_back(i);
   char uname[96];
-  std::snprintf(uname, sizeof(uname), "uniform: %u stripes, 2 lost, rs_apply_perm<%u,2>", N, k);
+  const uint32_t un = c2 ? uint32_t(hist[1]) : N;
+  std::snprintf(uname, sizeof(uname), "uniform: %u stripes, %u lost, rs_apply_perm<%u,%u>", un, ul,
+                k, ul);
   if (timeit(uname, [&] {
-        storb_rs_decode_batch_dev(ctx, k, n, B, N, s2.data(), k, d, 0, p, 0, d, 0, st[0]);
-      }, double(N) * (k + 2) * B))
+        storb_rs_decode_batch_dev(ctx, k, n, B, un, s2.data(), k, d, 0, p, 0, d, 0, st[0]);
+      }, double(un) * (k + ul) * B))
     return 1;
   storb_rs_ctx_destroy(ctx);
   return 0;
