@@ -52,6 +52,13 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   // measured. From pageable chunks the SDMA pipeline stays ahead (34 vs
   // 20 GiB/s: the host's packing competes with the kernel's reads of the
   // same staging), and the hashed path keeps the shares on the device.
+  // Piece ids from the encode kernel itself (rs_encode_hash.hip) where the
+  // geometry has one: digests land in [c][n] order. Not zero-copy: run on
+  // page-locked chunks over PCIe (its lanes read 64-byte pieces 1 KiB
+  // apart) it gave 30.9-33.0 GiB/s against 32.9 staged
+  // (profiles/r4r_hashed_zc.txt).
+  const bool fused = hashes_out && p > 0 && ctx->fused_hash && S == B &&
+                     encode_hash_supported(k, n, B);
   const bool zc = ctx->zc_batch && !hashes_out && p > 0 && in_direct;
   DeviceGuard g(ctx->device);
   for (int b = 0; b < 2; b++) {
@@ -61,10 +68,6 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
       HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(n) * S * batch + hash_bytes));
   }
   const uint32_t nb = (nchunks + batch - 1) / batch;
-  // Piece ids from the encode kernel itself (rs_encode_hash.hip) where the
-  // geometry has one: digests land in [c][n] order.
-  const bool fused = hashes_out && p > 0 && ctx->fused_hash && S == B &&
-                     encode_hash_supported(k, n, B);
   HostPool &pool = host_pool(ctx);
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;

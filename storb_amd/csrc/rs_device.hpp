@@ -408,7 +408,22 @@ __device__ __forceinline__ void desc_body(const DescArgs &a, cu64 *rec, uint32_t
   typedef const PermTab __attribute__((address_space(4))) cPermTab;
   cPermTab *gtabs = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
   const DescView v{rec, a.k, a.r};
-  auto run = [&](auto tabs0) {
+  auto run = [&](auto tabs0) __attribute__((always_inline)) {
+    if constexpr (RM > 8) {
+      // 9-16 rebuilt rows: one guarded tile shape for every case. With the
+      // four shapes below (one tile / loop, guarded / not) the body was too
+      // large to inline at k = 32, and the out-of-line copy the compiler
+      // made instead (every uniform value in VGPRs, flat loads of the
+      // captures) never finished on a 16-byte share (tools/fuzz.py seed
+      // 4242; tests/test_gpu_patterns.py::test_decode_chunks_tiny_shares_many_lost).
+      for (uint32_t t = t0; t < t1; t++) {
+        uint32_t zero = 0;
+        asm volatile("" : "+s"(zero));
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs0 + zero, a.k, r, cols,
+                                                         t * TILE + threadIdx.x);
+      }
+      return;
+    }
     if (a.tpw == 1) {  // one tile (desc_tpw's choice unless the grid is huge): no loop
       const uint32_t base = t0 * TILE;
       if (base + TILE <= cols)

@@ -103,6 +103,15 @@ def test_no_device_is_an_error_not_a_fallback():
     assert e.value.code == _lib.ENODEV
 
 
+def test_device_numa_node_without_a_device():
+    """storb_rs_device_numa_node: -1 for a device that is not there (it reads
+    sysfs through the device's PCI bus id; nothing to read without one)."""
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is present")
+    assert _lib.lib().storb_rs_device_numa_node(0) == -1
+    assert _lib.lib().storb_rs_device_numa_node(7) == -1
+
+
 def test_jit_compiles_decode_kernels_without_gpu():
     """The run-time-compiled decode kernels build with hipRTC on the host
     (no GPU): RS(16,8) with every data share lost, in place and assembled,

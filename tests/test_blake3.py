@@ -221,3 +221,32 @@ def test_device_batch_rejects_oversize(ctx):
     with pytest.raises(_lib.StorbRsError) as e:
         ctx.blake3_batch_dev(0, (16 << 20) + 1, 1, 0, 0)
     assert e.value.code == _lib.EINVAL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned_out", [True, False])
+def test_encode_chunks_hashed_zero_copy(ctx, pinned_out):
+    """storb_rs_encode_chunks_hashed from page-locked chunks (DMA'd in place,
+    parity written in place when the output is page-locked too, else through
+    staging), the fused kernel on the device: oracle parity, host blake3 of
+    every share."""
+    from oracle import coracle
+    k, n, L, N = 4, 6, 1 << 20, 5
+    B = L // k
+    src = _lib.PinnedBuffer(N * L)
+    src.array[:] = np.frombuffer(np.random.default_rng(77).bytes(N * L), dtype=np.uint8)
+    if pinned_out:
+        dst = _lib.PinnedBuffer(N * (n - k) * B)
+        out = dst.array
+    else:
+        out = np.empty(N * (n - k) * B, np.uint8)
+    out[:] = 0
+    ids = np.zeros((N, n, 32), np.uint8)
+    par, ids = ctx.encode_chunks_hashed(k, n, src.array, L, N, out=out, hashes=ids)
+    for c in range(N):
+        shares, _, _ = coracle.encode(k, n, src.array[c * L:(c + 1) * L])
+        for i in range(k, n):
+            o = (c * (n - k) + i - k) * B
+            assert np.array_equal(par[o:o + B], shares[i]), (c, i)
+        for t in range(n):
+            assert ids[c, t].tobytes() == _lib.blake3(shares[t].tobytes()), (c, t)

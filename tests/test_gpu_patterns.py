@@ -209,3 +209,62 @@ def test_decode_chunks_each_chunk_in_its_own_registered_buffer():
     (tests/registered_ranges.py)."""
     from test_gpu_runtime import run_registered_case
     run_registered_case("each_chunk_own_range")
+
+
+def _lose(k, n, e, rng):
+    """Survivor ids of a stripe that lost e random data shares: the other
+    data shares and the first e parity shares, shuffled."""
+    lost = set(rng.sample(range(k), e))
+    ids = [j for j in range(k) if j not in lost] + list(range(k, k + e))
+    rng.shuffle(ids)
+    return ids
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n", [(16, 24), (32, 48)])
+@pytest.mark.parametrize("inplace", [True, False])
+def test_decode_stripes_dev_many_lost_rows(ctx, k, n, inplace):
+    """Stripes that lost 5-16 data shares each: one descriptor launch per
+    rebuilt-row count above the mixed launch's four (rs_apply_desc<k, 5..8>
+    and the 16-row bucket for 9-16), in place and into a separate buffer
+    (fused assembly), oracle-exact."""
+    B, ns = 4096, 48
+    rng = random.Random(k + inplace)
+    data, par = oracle_stripes(k, n, B, ns, 5 * k + inplace)
+    sets = [_lose(k, n, 5 + s % (min(k, n - k) - 4), rng) for s in range(ns)]
+    dd = torch.from_numpy(data.copy()).to(DEV)
+    dp = torch.from_numpy(par.copy()).to(DEV)
+    view = dd.view(ns, k, B)
+    for s, ids in enumerate(sets):
+        for j in range(k):
+            if j not in ids:
+                view[s, j].fill_(0xA5)
+    out = dd if inplace else torch.full_like(dd, 0x3C)
+    ctx.decode_stripes_dev(k, n, B, sets, dd.data_ptr(), dp.data_ptr(), out.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(ns, k, B)
+    for s in range(ns):
+        assert np.array_equal(got[s], data[s]), (k, s, sorted(sets[s]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [17, 32 * 16, 32 * 17 + 3])
+def test_decode_chunks_tiny_shares_many_lost(ctx, L):
+    """storb_rs_decode_chunks at k = 32 with 1-18-byte shares (16-byte staged
+    rows, one column) and 16 / 10 / 7 rebuilt rows per chunk: the case
+    tools/fuzz.py (seed 4242) found waiting forever on the 9-16-row
+    descriptor kernel, now one guarded tile shape (rs_device.hpp desc_body)."""
+    k, n = 32, 48
+    ids_all = [list(range(16, 48)),
+               [13, 46, 39, 29, 12, 47, 41, 3, 18, 22, 44, 17, 8, 43, 25, 20, 9, 45, 5, 36, 0, 14,
+                7, 2, 26, 37, 21, 27, 23, 35, 40, 16, 19, 33],
+               [13, 25, 45, 46, 5, 15, 11, 30, 37, 44, 14, 16, 2, 21, 29, 33, 3, 47, 28, 34, 41,
+                17, 32, 1, 23, 8, 0, 36, 38, 19, 39, 26, 12, 10, 42, 27, 40, 9, 7]]
+    objs = [rnd(L, 90 + c) for c in range(3)]
+    batch = []
+    for c, o in enumerate(objs):
+        sh, B, pad = coracle.encode(k, n, o)
+        batch.append(([sh[i] for i in ids_all[c]], ids_all[c]))
+    got = ctx.decode_chunks(k, n, B, pad, batch)
+    for c in range(3):
+        assert np.array_equal(got[c], objs[c]), (L, c)

@@ -6,7 +6,8 @@ Each round draws a geometry ((k, n) from Storb's sizings plus odd ones), a
 chunk length (1 byte .. 6 MiB, ragged), an entry point (single encode /
 decode / repair, batched encode_chunks[_hashed] / decode_chunks (page-locked:
 scattered or arena shares, decoded in place), device
-batched encode / decode / repair) and page-locked or pageable buffers, and
+batched encode / decode / repair / encode with piece ids) and page-locked or
+pageable buffers, and
 compares the result byte for byte with the oracle. Runs for --seconds and
 prints one JSON line; exits non-zero on the first mismatch.
 
@@ -47,19 +48,25 @@ def check(cond, what):
         raise AssertionError(what)
 
 
+TRACE = None  # --trace FILE: each round's tag, written before it runs
+
+
 def one(ctx, rng, stats):
     k, n = rng.choice(GEOS)
     L = rng.choice([1, 15, 16, 17, 4095, 65536, 65537, (1 << 20) - 3, 3 << 20,
-                    rng.randint(1, 6 << 20)])
+                    rng.randint(1, 6 << 20), 1 << 20, 256 << 10])
     L = max(L, 1)
     data = rnd(rng, L)
     shares, B, pad = coracle.encode(k, n, data)
     keep = []
     pin = rng.random() < 0.4
     api = rng.choice(["encode", "decode", "repair", "encode_chunks", "hashed", "decode_chunks",
-                      "dev_encode", "dev_decode", "dev_repair"])
+                      "dev_encode", "dev_decode", "dev_repair", "dev_hashed"])
     stats[api] = stats.get(api, 0) + 1
     tag = f"{api} k={k} n={n} L={L} pinned={pin}"
+    if TRACE:
+        TRACE.write(tag + "\n")
+        TRACE.flush()
     if api == "encode":
         src = pinned_copy(data, keep) if pin else data
         par = [pinned_copy(np.zeros(B, np.uint8), keep) if pin else np.zeros(B, np.uint8)
@@ -127,6 +134,34 @@ def one(ctx, rng, stats):
         got = ctx.decode_chunks(k, n, B, pad, batch, out=out)
         check(all(np.array_equal(got[c], objs[c]) for c in range(cnt)),
               tag + f" cnt={cnt} arena={arena}")
+    elif api == "dev_hashed":
+        # storb_rs_encode_hashed_dev: the fused kernel for (2, 3) / (4, 6)
+        # with whole-KiB shares up to 256 KiB, two kernels otherwise
+        if n == k:
+            return
+        ns = rng.randint(1, 40)
+        Bd = rng.choice([1024, 2048, 3072, 5 << 10, 64 << 10, 255 << 10, 256 << 10, 1000, 16,
+                         512 << 10])
+        if ns * n * Bd > (64 << 20):
+            ns = max(1, (64 << 20) // (n * Bd))
+        pad_d = rng.choice([0, 0, 16, 4096])
+        ds, ps = k * Bd + pad_d, (n - k) * Bd + pad_d
+        host = rnd(rng, ns * ds)
+        d = torch.from_numpy(host).cuda()
+        p = torch.zeros(ns * ps, dtype=torch.uint8, device="cuda")
+        h = torch.zeros(ns * n * 32, dtype=torch.uint8, device="cuda")
+        ctx.encode_hashed_dev(k, n, Bd, ns, d.data_ptr(), p.data_ptr(), h.data_ptr(),
+                              ds if pad_d else 0, ps if pad_d else 0)
+        ctx.sync()
+        par, ids = p.cpu().numpy(), h.cpu().numpy().reshape(ns, n, 32)
+        for s_ in sorted({0, ns - 1, rng.randrange(ns)}):
+            sh = coracle.encode(k, n, host[s_ * ds:s_ * ds + k * Bd])[0]
+            for i in range(k, n):
+                o = s_ * ps + (i - k) * Bd
+                check(np.array_equal(par[o:o + Bd], sh[i]), tag + f" hashed_dev s={s_} i={i} B={Bd}")
+            for t in range(n):
+                check(ids[s_, t].tobytes() == _lib.blake3(sh[t].tobytes()),
+                      tag + f" hashed_dev id s={s_} t={t} B={Bd}")
     else:
         ns = rng.randint(1, 6)
         Bd = rng.choice([16, 1024, 4096 + 16, 32 << 10, B - B % 16 or 16])
@@ -167,7 +202,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=60)
     ap.add_argument("--seed", type=int, default=int(time.time()) & 0xFFFF)
+    ap.add_argument("--trace", default=None)
     a = ap.parse_args()
+    global TRACE
+    if a.trace:
+        TRACE = open(a.trace, "a")
     rng = random.Random(a.seed)
     ctx = _lib.Context(0)
     ctx.default_stream = torch.cuda.current_stream(0).cuda_stream
