@@ -163,3 +163,25 @@ def test_exit_with_jit_compiles_in_flight():
                        timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "queued" in r.stdout
+
+
+def test_device_kernels_make_no_function_calls(tmp_path):
+    """Every gfx950 kernel in the library is one inlined body: no s_swappc.
+    An out-of-line call is how the 9-16-row descriptor kernel at k = 32 once
+    compiled (uniform values in VGPRs, captures read through flat loads) --
+    and it never finished on a 16-byte share (tools/fuzz.py seed 4242)."""
+    import glob
+    import shutil
+    llvm = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(llvm):
+        pytest.skip("llvm-objdump not installed")
+    lib = tmp_path / "libstorb_rs.so"
+    shutil.copy(_lib.LIB_PATH, lib)
+    subprocess.run([llvm, "--offloading", str(lib)], cwd=tmp_path, check=True,
+                   capture_output=True)
+    objs = sorted(glob.glob(str(tmp_path / "*hipv4-amdgcn-amd-amdhsa--gfx950")))
+    assert objs, "no gfx950 code objects in the library"
+    for o in objs:
+        dis = subprocess.run([llvm, "-d", "--mcpu=gfx950", o], capture_output=True, text=True,
+                             check=True).stdout
+        assert "s_swappc" not in dis, os.path.basename(o)
