@@ -63,11 +63,14 @@ __device__ __forceinline__ PermTab eh_tab(const EncHashArgs &a, int j, int i) {
   return p;
 }
 
-// Chunk-phase shape (tools/ehbench.hip sweeps it): PF = the next block of
-// data shares is loaded before the current ones are compressed; GS = shares
-// compressed together in one basic block (GS = 2: two independent
-// compressions for the scheduler to interleave); CVL = the chaining values
-// live in LDS (the tree's area) instead of N x 8 VGPRs.
+// Chunk-phase shape (tools/ehbench.hip sweeps it). PF: 0 = each data block
+// loaded right before it is folded, 1 = the next group's blocks loaded
+// before the current group is compressed, 2 = rolling, share j's next block
+// loaded right after its current one is compressed (before the step's
+// parity stores). GS = shares compressed together in one basic block (2:
+// two independent compressions for the scheduler to interleave; PF < 2).
+// CVL = the chaining values live in LDS (the tree's area) instead of N x 8
+// VGPRs. ST: 0 = non-temporal parity stores, 1 = write-back.
 template <int K, int M, int PF, int GS, bool CVL, int DIAG = 0, int ST = 0>
 __global__ __launch_bounds__(kEHThreads) void rs_encode_hash(const EncHashArgs a) {
   // DIAG (tools/ehbench.hip only, wrong output): 1 = no GF fold, 2 = no
