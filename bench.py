@@ -132,6 +132,63 @@ def _cpu_where(cpu):
     return {"cpu": cpu, "cpu_mhz": mhz, "numa_node": node}
 
 
+def _ssbd_run(run, secs):
+    """run(fresh=True, secs) on a fresh thread that first turns SSBD on for
+    itself (PR_SET_SPECULATION_CTRL; irreversible for that thread only)."""
+    import ctypes
+    import threading
+    res = {}
+
+    def body():
+        libc = ctypes.CDLL(None, use_errno=True)
+        rc = libc.prctl(53, 0, 4, 0, 0)  # PR_SET_SPECULATION_CTRL, PR_SPEC_STORE_BYPASS, DISABLE
+        if rc != 0:
+            res["refused_errno"] = ctypes.get_errno()
+            return
+        v, c, e, a = run(True, secs)
+        res.update({"value": v, "unit": "GiB/s", "calls": c, "seconds": round(e, 2),
+                    "ipc": a.get("ipc"), "effective_ghz": a.get("effective_ghz"),
+                    "l1_addmul_GBps": a.get("l1_addmul_GBps"),
+                    "Speculation_Store_Bypass": a["speculation"].get("Speculation_Store_Bypass")})
+
+    t = threading.Thread(target=body)
+    t.start()
+    t.join()
+    return res
+
+
+def _speculation_state():
+    """The measuring thread's speculative-store-bypass state and seccomp mode
+    (/proc/thread-self/status) and the kernel's global view (sysfs). With
+    SSBD on (e.g. forced for every seccomp-filtered process, the kernel's
+    default `spec_store_bypass_disable=seccomp`), a load waits for every
+    older store's address: the oracle's byte-wise read-modify-write loop is
+    exactly that pattern, while register-only and streaming-read code is not
+    affected."""
+    out = {}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("microcode"):
+                out["microcode"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        for line in open("/proc/thread-self/status"):
+            key = line.split(":")[0]
+            if key in ("Speculation_Store_Bypass", "SpeculationIndirectBranch", "Seccomp",
+                       "Seccomp_filters"):
+                out[key] = line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    try:
+        out["vulnerabilities_spec_store_bypass"] = open(
+            "/sys/devices/system/cpu/vulnerabilities/spec_store_bypass").read().strip()
+    except OSError:
+        pass
+    return out
+
+
 def _proc_stat():
     """Per-CPU jiffies from /proc/stat: {cpu: (total, steal)}."""
     out = {}
@@ -202,13 +259,15 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
                 **_cpu_where(r["cpu_start"]),
                 # time the hypervisor ran something else on this vCPU: the
                 # thread's own CPU time does not show it (/proc/stat steal)
-                "cpu_steal_frac": _steal_frac(st0, st1, r["cpu_start"])}
+                "cpu_steal_frac": _steal_frac(st0, st1, r["cpu_start"]),
+                "speculation": _speculation_state()}
         if r["cpu_end"] != r["cpu_start"]:
             acct["cpu_end"] = r["cpu_end"]
         return round(legs * r["calls"] * chunk_bytes / GIB / el, 4), r["calls"], el, acct
 
     value, calls, el, acct = run(True, seconds)
     arith, acalls, ael, aacct = run(False, max(1.0, seconds / 2))
+    ssbd = _ssbd_run(run, max(1.0, seconds / 4))
     shape = (f"{chunk_bytes >> 10} KiB chunks (k={k},n={n}"
              f"{', erased ' + (str(sorted(erased)) if not survivor_sets else 'per chunk (download patterns)') if do_decode else ''})")
     return {
@@ -223,6 +282,13 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
         "arithmetic_only": {"value": arith, "unit": "GiB/s",
                             "sample": f"{acalls} x {what}, {ael:.1f} s, buffers allocated once",
                             "thread": aacct},
+        # the same loop on a thread with Speculative Store Bypass Disable on
+        # (prctl, that thread only): on some boxes of this pool the oracle's
+        # byte-wise read-modify-write loop runs ~19x slower with store-bypass
+        # speculation enabled (IPC 0.16 vs 3.06, tools/ssbd_probe.py,
+        # DESIGN.md §5 Host variance); `value` stays the process as started,
+        # as the reference would run
+        "ssbd_on": ssbd,
     }
 
 
