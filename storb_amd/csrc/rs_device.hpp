@@ -394,13 +394,44 @@ __global__ __launch_bounds__(T) void rs_apply_perm(const ApplyArgs a) {
 // rs_apply_perm does over `tpw` consecutive tiles of the stripe: the record
 // -> tables -> first loads chain (~1-2 us of dependent latency a workgroup
 // of one tile pays before its first byte streams) is paid once per tpw tiles.
+// ONE (the mixed launch): exactly one tile per workgroup, the launcher
+// refuses tpw != 1, and without COPY the row count is the branch's own
+// compile-time RM -- no tile loop or run-time row guards in the code, which
+// held the mixed kernel 1-2 % below the same tile without them
+// (tools/mixbench.hip "same shape here").
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL, bool PAIR, bool COPY,
-          int RL = RM>
+          int RL = RM, bool ONE = false>
 __device__ __forceinline__ void desc_body(const DescArgs &a, cu64 *rec, uint32_t r,
                                           PermTab *lds_ptab) {
   constexpr uint32_t TILE = T * U;
   const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
   const uint32_t tps = (cols + TILE - 1) / TILE;
+  if constexpr (ONE) {
+    typedef const PermTab __attribute__((address_space(4))) cPermTab;
+    cPermTab *gt = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
+    const DescView v{rec, a.k, a.r};
+    const uint32_t base = (blockIdx.x % tps) * TILE;
+    const uint32_t rr = COPY ? r : static_cast<uint32_t>(RM);
+    auto go = [&](auto tabs) __attribute__((always_inline)) {
+      if (base + TILE <= cols)
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, rr, cols,
+                                                          base + threadIdx.x);
+      else
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, rr, cols,
+                                                         base + threadIdx.x);
+    };
+    if constexpr (TL) {
+      const uint32_t n16 = (COPY && r == 0) ? 0u : a.k * RM * (sizeof(PermTab) / 16);
+      typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
+      for (uint32_t t = threadIdx.x; t < n16; t += T)
+        reinterpret_cast<u32x4 *>(lds_ptab)[t] = ((gcu32x4 *)(gt))[t];
+      __syncthreads();
+      go(static_cast<const PermTab *>(lds_ptab));
+    } else {
+      go(gt);
+    }
+    return;
+  }
   const uint32_t wps = (tps + a.tpw - 1) / a.tpw;  // workgroups per stripe
   const uint32_t item = blockIdx.x / wps;
   const uint32_t t0 = (blockIdx.x - item * wps) * a.tpw;
@@ -498,15 +529,15 @@ __global__ __launch_bounds__(kThreads) void rs_apply_desc_mix(const DescArgs a) 
   using T1 = Tune<KM, 1>;
   __shared__ __attribute__((aligned(16))) PermTab lds_ptab[T1::TL ? KM * kMixR : 1];
   const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + kThreads - 1) / kThreads;
-  const uint32_t item = blockIdx.x / ((tps + a.tpw - 1) / a.tpw);
+  const uint32_t item = blockIdx.x / tps;  // one tile per workgroup (launch_desc_mix)
   cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
   const uint32_t r = static_cast<uint32_t>(rec[0] >> 32);
 #define STORB_MIX_CASE(R)                                                                   \
   {                                                                                         \
     using C = Tune<KM, R>;                                                                  \
     static_assert(C::T == kThreads && C::U == 1, "mixed launch: one tile shape");           \
-    desc_body<KM, R, C::T, C::U, C::BAR, mix_g<KM, R>(), C::TL, mix_pair<KM, R>(), COPY>(   \
-        a, rec, r, lds_ptab);                                                               \
+    desc_body<KM, R, C::T, C::U, C::BAR, mix_g<KM, R>(), C::TL, mix_pair<KM, R>(), COPY, R, \
+              true>(a, rec, r, lds_ptab);                                                   \
     return;                                                                                 \
   }
   if (r <= 1) STORB_MIX_CASE(1)
@@ -620,7 +651,7 @@ template <int KM>
 hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
   constexpr uint64_t TILE = kThreads;
   const uint64_t tps = ((a.block >> 4) + TILE - 1) / TILE;
-  if (a.tpw == 0) return hipErrorInvalidValue;
+  if (a.tpw != 1) return hipErrorInvalidConfiguration;  // one tile per workgroup
   const uint64_t blocks = ((tps + a.tpw - 1) / a.tpw) * a.nitems;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;

@@ -96,9 +96,11 @@ __device__ __forceinline__ void vbody(const DescArgs &a, const Bounds &b, cu64 *
   }
 }
 
-// Paired inputs per branch: PSET 0 none, 1 all, 2 R <= 3, 3 R <= 2.
+// Paired inputs per branch: PSET 0 none, 1 all, 2 R <= 3, 3 R <= 2, 4 R != 2,
+// 5 R >= 3, 6 R == 1.
 constexpr bool psel(int PSET, int R) {
-  return PSET == 1 || (PSET == 2 && R <= 3) || (PSET == 3 && R <= 2);
+  return PSET == 1 || (PSET == 2 && R <= 3) || (PSET == 3 && R <= 2) || (PSET == 4 && R != 2) ||
+         (PSET == 5 && R >= 3) || (PSET == 6 && R == 1);
 }
 
 template <int KM, int G, bool TL, bool SORTED, bool INL, int U = 1, int GSET = 0,
@@ -161,6 +163,10 @@ std::vector<Var> variants() {
     v.push_back(mk<KM, 4, true, false, false, 1, 0, 1>("G4 PAIR all", 0));
     v.push_back(mk<KM, 4, true, false, false, 1, 0, 2>("G4 PAIR R<=3", 0));
     v.push_back(mk<KM, 8, true, false, false, 1, 1, 1>("GSET1 PAIR all", 0));
+    v.push_back(mk<KM, 8, true, false, false, 1, 0, 4>("G8 PAIR R!=2", 0));
+    v.push_back(mk<KM, 8, true, false, false, 1, 0, 5>("G8 PAIR R>=3", 0));
+    v.push_back(mk<KM, 8, true, false, false, 1, 0, 6>("G8 PAIR R==1", 0));
+    v.push_back(mk<KM, 8, true, false, false, 1, 0, 1>("G8 PAIR all (again)", 0));
   } else {
     v.push_back(mk<KM, 16, true, false, false>("G16 (TL, rec[0])", 0));
     v.push_back(mk<KM, 16, true, false, false>("G16 cap3", 3));
