@@ -94,6 +94,7 @@ extern "C" {
     fn storb_rs_host_register(p: *mut c_void, len: usize) -> c_int;
     fn storb_rs_host_unregister(p: *mut c_void) -> c_int;
     fn storb_blake3(data: *const u8, len: usize, out: *mut u8);
+    fn storb_rs_device_numa_node(device: c_int) -> c_int;
 }
 
 // glibc, for the ops' wake-up descriptors (tokio AsyncFd / epoll).
@@ -118,6 +119,20 @@ pub fn blake3(data: &[u8]) -> [u8; 32] {
     let mut out = [0u8; 32];
     unsafe { storb_blake3(data.as_ptr(), data.len(), out.as_mut_ptr()) };
     out
+}
+
+/// NUMA node of the host socket GPU `device` hangs off (None if unknown).
+/// Per-chunk calls from a thread on another socket pay the socket link
+/// ((4, 6) 1 MiB encode 59.5 vs 51.4 us): run the upload /
+/// download workers on this node's CPUs (`/sys/devices/system/node/node<N>/cpulist`,
+/// e.g. from a tokio runtime's `on_thread_start`).
+pub fn device_numa_node(device: i32) -> Option<u32> {
+    let n = unsafe { storb_rs_device_numa_node(device) };
+    if n < 0 {
+        None
+    } else {
+        Some(n as u32)
+    }
 }
 
 /// A GPU context: streams, staging, table caches. Calls on one context are
