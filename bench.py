@@ -292,7 +292,8 @@ def cpu_baseline(k, n, chunk_bytes, erased, seconds, do_encode=True, do_decode=T
     }
 
 
-def cpu_baseline_threads(k, n, chunk_bytes, erased, threads=16, nchunks=256, seconds=3.0):
+def cpu_baseline_threads(k, n, chunk_bytes, erased, threads=16, nchunks=256, seconds=3.0,
+                         ssbd=True):
     """The same CPU path on `threads` host threads over independent chunks
     ("nproc threads on independent chunks"; 16 = this box's
     CPU share per GPU). Encode + decode round trips over `nchunks` distinct
@@ -311,10 +312,29 @@ def cpu_baseline_threads(k, n, chunk_bytes, erased, threads=16, nchunks=256, sec
         if time.perf_counter() - t0 >= seconds:
             break
     el = time.perf_counter() - t0
-    return {"value": round(2 * passes * nchunks * chunk_bytes / GIB / el, 4), "unit": "GiB/s",
-            "cores": threads, "kind": "port",
-            "sample": f"{passes} passes x {nchunks} x encode+decode of {chunk_bytes >> 10} KiB "
-                      f"chunks, {threads} threads, {el:.2f} s"}
+    res = {"value": round(2 * passes * nchunks * chunk_bytes / GIB / el, 4), "unit": "GiB/s",
+           "cores": threads, "kind": "port",
+           "sample": f"{passes} passes x {nchunks} x encode+decode of {chunk_bytes >> 10} KiB "
+                     f"chunks, {threads} threads, {el:.2f} s"}
+    if ssbd:
+        # the same from a thread with SSBD on: the C workers it starts inherit
+        # it (cpu_baseline's ssbd_on, DESIGN.md §5 Host variance)
+        import ctypes
+        import threading
+        out = {}
+
+        def body():
+            if ctypes.CDLL(None).prctl(53, 0, 4, 0, 0) != 0:
+                out["refused"] = True
+                return
+            out.update(cpu_baseline_threads(k, n, chunk_bytes, erased, threads, nchunks,
+                                            max(1.0, seconds / 2), ssbd=False))
+
+        t = threading.Thread(target=body)
+        t.start()
+        t.join()
+        res["ssbd_on"] = {x: out.get(x) for x in ("value", "sample", "refused") if x in out}
+    return res
 
 
 def cpu_quota():
