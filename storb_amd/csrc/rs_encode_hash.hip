@@ -116,7 +116,8 @@ __global__ __launch_bounds__(kEHThreads) void rs_encode_hash(const EncHashArgs a
     auto load_blk = [&](int j, uint32_t b, uint32_t *m) {
       // the four dwordx4 of a block share 128-B lines with the next block:
       // cached loads
-      const u32x4 *q = reinterpret_cast<const u32x4 *>(d + j * a.block + b * b3::kBlockLen);
+      const u32x4 *q =
+          reinterpret_cast<const u32x4 *>(d + j * a.share_stride + b * b3::kBlockLen);
 #pragma unroll
       for (int e = 0; e < 4; e++) {
         const u32x4 v = q[e];
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(kEHThreads) void rs_encode_hash(const EncHashArgs a
       for (int j = 0; j < K; j++) load_blk(j, 0, blk[j]);
       for (uint32_t b = 0; b < b3::kChunkLen / b3::kBlockLen; b++) {
         const uint32_t flags = (b == 0 ? b3::kChunkStart : 0u) | (b == 15 ? last_flags : 0u);
-        uint32_t par[M][16];
+        uint32_t par[M > 0 ? M : 1][16];  // (M = 0: hash only)
 #pragma unroll
         for (int i = 0; i < M; i++)
 #pragma unroll
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(kEHThreads) void rs_encode_hash(const EncHashArgs a
       for (int h = 0; h < GS; h++) load_blk(h, 0, cur[h]);
     for (uint32_t b = 0; b < b3::kChunkLen / b3::kBlockLen; b++) {
       const uint32_t flags = (b == 0 ? b3::kChunkStart : 0u) | (b == 15 ? last_flags : 0u);
-      uint32_t par[M][16];
+      uint32_t par[M > 0 ? M : 1][16];  // (M = 0: hash only)
 #pragma unroll
       for (int i = 0; i < M; i++)
 #pragma unroll

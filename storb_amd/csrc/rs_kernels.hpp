@@ -111,6 +111,7 @@ struct EncHashArgs {
   uint64_t parity_stride;
   uint8_t *hashes;
   uint64_t block;
+  uint64_t share_stride;  // data share j of a stripe at data + s*data_stride + j*share_stride
   uint32_t nstripes, nchunks, seg_log2, pad;
   uint32_t tab[kEHMaxTabs][5];  // [j*(n-k) + i]: perm_tab(parity coefficient)
 };

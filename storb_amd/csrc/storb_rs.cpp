@@ -998,6 +998,7 @@ bool try_encode_hash(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
   a.parity_stride = parity_stride;
   a.hashes = d_hashes;
   a.block = block;
+  a.share_stride = block;
   a.nstripes = nstripes;
   a.nchunks = static_cast<uint32_t>(block / 1024);
   while ((1u << a.seg_log2) < a.nchunks) a.seg_log2++;

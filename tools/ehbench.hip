@@ -47,6 +47,28 @@ struct V {
   bool diag = false;  // wrong output by design: timed, not compared
 };
 
+// Hash-only shapes of the same kernel (M = 0): the stripes' data shares then
+// parity shares as B-pitched messages, G per lane (messages past the last
+// whole group are skipped: timing only).
+template <int G, int PF>
+hipError_t hash_only(const EncHashArgs &e, int K, int M, hipStream_t s) {
+  auto run = [&](const uint8_t *in, uint32_t count, uint8_t *out) {
+    EncHashArgs a{};
+    a.data = in;
+    a.data_stride = uint64_t(G) * e.block;
+    a.share_stride = e.block;
+    a.hashes = out;
+    a.block = e.block;
+    a.nstripes = count / G;
+    a.nchunks = e.nchunks;
+    a.seg_log2 = e.seg_log2;
+    return a.nstripes ? launch_eh<G, 0, PF, 1, false, 0, 0>(a, s) : hipSuccess;
+  };
+  hipError_t r = run(e.data, e.nstripes * K, e.hashes + 4096);
+  if (r == hipSuccess) r = run(e.parity, e.nstripes * M, e.hashes + 4096 + size_t(e.nstripes) * K * 32);
+  return r;
+}
+
 template <int K, int M>
 std::vector<V> variants() {
   return {
@@ -69,6 +91,18 @@ std::vector<V> variants() {
       {"diag PF1 GS1: no GF fold", launch_eh<K, M, true, 1, false, 1>, {}, true},
       {"diag PF1 GS1: no parity stores", launch_eh<K, M, true, 1, false, 2>, {}, true},
       {"diag PF1 GS1: neither", launch_eh<K, M, true, 1, false, 3>, {}, true},
+      {"hash only, 4 per lane, PF2 write-back", [](const EncHashArgs &a, hipStream_t s) {
+         return hash_only<4, 2>(a, K, M, s);
+       }, {}, true},
+      {"hash only, 4 per lane, PF1", [](const EncHashArgs &a, hipStream_t s) {
+         return hash_only<4, 1>(a, K, M, s);
+       }, {}, true},
+      {"hash only, 6 per lane, PF1", [](const EncHashArgs &a, hipStream_t s) {
+         return hash_only<6, 1>(a, K, M, s);
+       }, {}, true},
+      {"hash only, 2 per lane, PF1", [](const EncHashArgs &a, hipStream_t s) {
+         return hash_only<2, 1>(a, K, M, s);
+       }, {}, true},
       {"reference: blake3_batch_kernel, all n shares", [](const EncHashArgs &a, hipStream_t s) {
          hipError_t e = launch_blake3_batch(a.data, a.block, a.nstripes * K, a.block,
                                             a.hashes + 4096, s);
@@ -96,6 +130,7 @@ int run(uint32_t N, size_t B, int L, int reps) {
   a.parity_stride = M * B;
   a.hashes = h;
   a.block = B;
+  a.share_stride = B;
   a.nstripes = N;
   a.nchunks = static_cast<uint32_t>(B / 1024);
   while ((1u << a.seg_log2) < a.nchunks) a.seg_log2++;
