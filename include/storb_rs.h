@@ -63,8 +63,18 @@ int storb_rs_device_count(void);
  * runtime places near the device): pin upload / download tasks there. */
 int storb_rs_device_numa_node(int device);
 /* device_ordinal >= 0 pins the context to that GPU; -1 picks devices
- * round-robin across contexts (objects partition across GPUs). */
+ * round-robin across contexts (objects partition across GPUs), among the GPUs
+ * on the calling thread's NUMA node when it has any (storb_rs_select_device;
+ * STORB_RS_NUMA_PICK=0 deals out all GPUs regardless of node). */
 int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out);
+/* The rule storb_rs_ctx_create(-1) applies, as a pure function (no device
+ * access; bindings and tests call it with any topology): the device that the
+ * `ticket`-th context of a thread on `caller_node` gets, given each device's
+ * node in device_nodes[0..ndev). Round-robin over the devices on caller_node;
+ * over all devices when the caller's node is unknown (< 0) or has none.
+ * -1 when ndev <= 0. */
+int storb_rs_select_device(int caller_node, const int *device_nodes, int ndev,
+                           uint64_t ticket);
 /* Waits for everything the context queued, returns its device memory
  * (stream-ordered pool memory included) and frees it. Async ops started on
  * it and not yet finished are waited for and detached: storb_rs_op_test and

@@ -95,6 +95,12 @@ extern "C" {
     fn storb_rs_host_unregister(p: *mut c_void) -> c_int;
     fn storb_blake3(data: *const u8, len: usize, out: *mut u8);
     fn storb_rs_device_numa_node(device: c_int) -> c_int;
+    fn storb_rs_select_device(
+        caller_node: c_int,
+        device_nodes: *const c_int,
+        ndev: c_int,
+        ticket: u64,
+    ) -> c_int;
 }
 
 // glibc, for the ops' wake-up descriptors (tokio AsyncFd / epoll).
@@ -132,6 +138,22 @@ pub fn device_numa_node(device: i32) -> Option<u32> {
         None
     } else {
         Some(n as u32)
+    }
+}
+
+/// The GPU `Context::new(-1)` gives the `ticket`-th context created by a
+/// thread on NUMA node `caller_node` (None: node unknown), for a topology
+/// given as each device's node: round-robin over the GPUs on the caller's
+/// socket, over all GPUs when that socket has none. Pure; no device access.
+pub fn select_device(caller_node: Option<u32>, device_nodes: &[i32], ticket: u64) -> Option<usize> {
+    let node = caller_node.map(|n| n as c_int).unwrap_or(-1);
+    let d = unsafe {
+        storb_rs_select_device(node, device_nodes.as_ptr(), device_nodes.len() as c_int, ticket)
+    };
+    if d < 0 {
+        None
+    } else {
+        Some(d as usize)
     }
 }
 

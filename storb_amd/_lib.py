@@ -119,6 +119,7 @@ def _declare(L):
     L.storb_blake3.restype = None
     L.storb_rs_blake3_batch_dev.argtypes = [vp, vp, sz, C.c_uint32, sz, vp, vp]
     L.storb_rs_device_numa_node.argtypes = [C.c_int]
+    L.storb_rs_select_device.argtypes = [C.c_int, C.POINTER(C.c_int), C.c_int, C.c_uint64]
     L.storb_rs_encode_hashed_dev.argtypes = [vp, C.c_uint32, C.c_uint32, sz, C.c_uint32,
                                              vp, sz, vp, sz, vp, vp]
     L.storb_rs_decode_chunks.argtypes = [vp, C.c_uint32, C.c_uint32, sz, sz, C.c_uint32,
@@ -170,6 +171,18 @@ def version() -> str:
 
 def device_count() -> int:
     return int(lib().storb_rs_device_count())
+
+
+def device_numa_node(device: int) -> int:
+    """NUMA node of the socket GPU `device` hangs off (-1 unknown)."""
+    return lib().storb_rs_device_numa_node(device)
+
+
+def select_device(caller_node: int, device_nodes: Sequence[int], ticket: int) -> int:
+    """The device storb_rs_ctx_create(-1) gives the ticket-th context of a
+    thread on NUMA node caller_node, for any topology (no device access)."""
+    arr = (C.c_int * max(1, len(device_nodes)))(*device_nodes)
+    return lib().storb_rs_select_device(caller_node, arr, len(device_nodes), ticket)
 
 
 def device_pool_stats(device: int = 0) -> tuple[int, int]:

@@ -69,6 +69,10 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   }
   const uint32_t nb = (nchunks + batch - 1) / batch;
   HostPool &pool = host_pool(ctx);
+  // Whether batch buffer b's digests came from the fused kernel (its [c][t]
+  // layout) or from the two hash launches ([c][j] data, then [c][i] parity):
+  // try_encode_hash may decline a batch the up-front check let through.
+  bool did_fuse[2] = {false, false};
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;
     const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
@@ -84,7 +88,7 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
         });
       }
     }
-    if (hashes_out && fused) {
+    if (hashes_out && did_fuse[b]) {
       std::memcpy(hashes_out + static_cast<size_t>(c0) * n * 32,
                   ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch,
                   static_cast<size_t>(cn) * n * 32);
@@ -150,8 +154,9 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     uint8_t *dh = dp + static_cast<size_t>(p) * S * batch;  // digests (if any)
     HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
     hipError_t fe = hipSuccess;
-    if (fused && try_encode_hash(ctx, k, n, B, cn, dd, per, dp, static_cast<size_t>(p) * S, dh,
-                                 s, &fe)) {
+    did_fuse[b] = fused && try_encode_hash(ctx, k, n, B, cn, dd, per, dp,
+                                           static_cast<size_t>(p) * S, dh, s, &fe);
+    if (did_fuse[b]) {
       HIP_TRY(ctx, fe);
     } else if (p > 0) {
       std::vector<const uint8_t *> in(k);
@@ -164,7 +169,7 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
       if (rc) return rc;
     }
     size_t back = static_cast<size_t>(p) * S * cn;
-    if (hashes_out && !fused) {
+    if (hashes_out && !did_fuse[b]) {
       // shares are pitched S apart across the whole batch: one launch each
       HIP_TRY(ctx, launch_blake3_batch(dd, B, cn * k, S, dh, s));
       if (p > 0)

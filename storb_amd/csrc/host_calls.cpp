@@ -302,11 +302,22 @@ extern "C" {
 // Staging for this call on the calling thread's NUMA node (ctx.hpp
 // pin_in_node): sched_getcpu is a vDSO read, the buffers are allocated once
 // per node and kept.
+// A thread that migrates between sockets would otherwise keep a staging pair
+// per node at its largest size; on a node switch the other nodes' buffers
+// above kStagingKeep are released (a (16, 24) 8 MiB chunk's 12 MiB pair stays).
+static constexpr size_t kStagingKeep = 16ull << 20;
+
 static void use_caller_staging(storb_rs_ctx *ctx) {
   int node = staging_node_env();
   if (node == -2) node = cpu_numa_node(sched_getcpu());
   const int slot = node >= 0 && node < storb_rs_ctx::kStagingNodes ? node
                                                                   : storb_rs_ctx::kStagingNodes;
+  if (ctx->pin_in != &ctx->pin_in_node[slot])
+    for (int i = 0; i <= storb_rs_ctx::kStagingNodes; i++) {
+      if (i == slot) continue;
+      if (ctx->pin_in_node[i].cap > kStagingKeep) ctx->pin_in_node[i].release();
+      if (ctx->pin_out_node[i].cap > kStagingKeep) ctx->pin_out_node[i].release();
+    }
   ctx->pin_in = &ctx->pin_in_node[slot];
   ctx->pin_out = &ctx->pin_out_node[slot];
   ctx->pin_node = slot < storb_rs_ctx::kStagingNodes ? node : -1;
@@ -332,7 +343,13 @@ static int encode_one(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint8_t *
       if (avail) dsegs.push_back({data_out[j], data + src, avail});
       if (B > avail) dsegs.push_back({data_out[j] + avail, nullptr, B - avail});
     }
+  // Runs once: a streamed call that gives up after its `during` step has
+  // copied the data shares retries on the sliced path, which must not copy
+  // the k * B bytes again.
+  bool data_put = false;
   const std::function<void()> put_data = [&] {
+    if (data_put) return;
+    data_put = true;
     if (!dsegs.empty()) host_pool(ctx).copy_segs(dsegs.data(), dsegs.size());
   };
   if (p == 0) {

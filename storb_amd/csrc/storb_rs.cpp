@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cctype>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -53,9 +54,23 @@ const std::vector<uint8_t> &cached_enc(uint32_t k, uint32_t n) {
   return it->second;
 }
 
-static std::atomic<int> g_rr{0};
+// Round-robin counters of storb_rs_ctx_create(-1): one per NUMA node of the
+// calling thread (a node's threads deal out that node's GPUs), the last for
+// callers whose node is unknown or has no GPU (they deal out all GPUs).
+static constexpr int kRrNodes = 64;
+static std::atomic<unsigned long long> g_rr[kRrNodes + 1];
 
-int next_round_robin() { return g_rr.fetch_add(1); }
+int next_round_robin() { return static_cast<int>(g_rr[kRrNodes].fetch_add(1) & 0x7fffffff); }
+
+// NUMA node of every visible device, read once (sysfs; -1 unknown).
+static const std::vector<int> &device_nodes() {
+  static const std::vector<int> nodes = [] {
+    std::vector<int> v(std::max(0, storb_rs_device_count()));
+    for (size_t d = 0; d < v.size(); d++) v[d] = storb_rs_device_numa_node(static_cast<int>(d));
+    return v;
+  }();
+  return nodes;
+}
 
 // Page-locked host ranges the caller obtained through storb_rs_host_alloc or
 // storb_rs_host_register. The pipelined host path DMAs straight from / into
@@ -86,8 +101,10 @@ Variant pick_variant(const storb_rs_ctx *ctx) {
 // that read the table on every stream that used it.
 // Give a table's device memory back to the stream-ordered pool it came from
 // (hipMallocAsync), ordered on ctx->stream after its upload and its last
-// use on every stream. Never hipFree: that is not the pool's free (a plain
-// hipFree of pool memory was what context teardown did until round 3).
+// use on every stream. Every table free in this file is a hipFreeAsync, the
+// pool's own free; a plain hipFree of pool memory (what context teardown did
+// until round 3) is legal only after a device-wide synchronisation and is
+// not used.
 static hipError_t release_table(storb_rs_ctx *ctx, Tables *t) {
   if (!t->dev) return hipSuccess;
   hipError_t e = hipStreamWaitEvent(ctx->stream, t->uploaded, 0);
@@ -198,7 +215,12 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
   e = hipMemcpyAsync(t->dev, host.data(), host.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipEventRecord(t->uploaded, s);
   if (e != hipSuccess) {
-    (void)hipStreamSynchronize(s);  // nothing may still read or write t's memory
+    // Nothing may still read or write t's memory; then give it back to its
+    // pool (stream-ordered, as every table free) before t goes away.
+    (void)hipStreamSynchronize(s);
+    (void)hipFreeAsync(t->dev, s);
+    (void)hipStreamSynchronize(s);
+    t->dev = nullptr;
     return hip_fail(ctx, e, "upload tables");
   }
   t->home = s;
@@ -581,13 +603,42 @@ int storb_rs_device_numa_node(int device) {
   return node;
 }
 
+int storb_rs_select_device(int caller_node, const int *device_nodes, int ndev,
+                           uint64_t ticket) {
+  if (ndev <= 0 || !device_nodes) return -1;
+  int local = 0;
+  if (caller_node >= 0)
+    for (int d = 0; d < ndev; d++) local += device_nodes[d] == caller_node;
+  if (local == 0) return static_cast<int>(ticket % static_cast<unsigned long long>(ndev));
+  unsigned long long want = ticket % static_cast<unsigned long long>(local);
+  for (int d = 0; d < ndev; d++)
+    if (device_nodes[d] == caller_node && want-- == 0) return d;
+  return -1;  // unreachable
+}
+
 int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   if (!out) return STORB_RS_EINVAL;
   *out = nullptr;
   const int ndev = storb_rs_device_count();
   if (ndev <= 0) return STORB_RS_ENODEV;
   int dev = device_ordinal;
-  if (dev < 0) dev = next_round_robin() % ndev;
+  if (dev < 0) {
+    // Round-robin over the GPUs on the calling thread's socket (upload.rs:
+    // 418-420's task reaches the context through the shim's thread-local,
+    // lib.rs:97-114): a context on the other socket's GPU pays the socket
+    // link on every staged call (58.4 vs 53.3 us per (4, 6) 1 MiB encode,
+    // BENCH_r04 shim_path.numa). STORB_RS_NUMA_PICK=0: plain round-robin.
+    const char *e = std::getenv("STORB_RS_NUMA_PICK");
+    const bool numa = !(e && std::atoi(e) == 0);
+    const std::vector<int> &nodes = device_nodes();
+    int node = numa ? cpu_numa_node(sched_getcpu()) : -1;
+    int local = 0;
+    if (node >= 0 && node < kRrNodes)
+      for (int x : nodes) local += x == node;
+    const int ctr = local ? node : kRrNodes;
+    dev = storb_rs_select_device(local ? node : -1, nodes.data(), ndev, g_rr[ctr].fetch_add(1));
+    if (dev < 0) return STORB_RS_ENODEV;
+  }
   if (dev >= ndev) return STORB_RS_EINVAL;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return STORB_RS_ENODEV;
@@ -632,18 +683,19 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     for (auto &kv : ctx->tables) (void)release_table(ctx, kv.second.get());
     (void)hipStreamSynchronize(ctx->stream);
   }
-  // A table whose stream-ordered release failed: free it once nothing on the
-  // device can still read it (hipFree of pool memory after a device-wide
-  // synchronisation returns it to its pool).
+  // A table whose stream-ordered release failed: once nothing on the device
+  // can still read it, free it on the null stream (still the pool's own
+  // free, hipFreeAsync) and wait for that.
   bool leftover = false;
   for (auto &kv : ctx->tables) leftover = leftover || kv.second->dev;
   if (leftover) {
     (void)hipDeviceSynchronize();
     for (auto &kv : ctx->tables)
       if (kv.second->dev) {
-        (void)hipFree(kv.second->dev);
+        (void)hipFreeAsync(kv.second->dev, nullptr);
         kv.second->dev = nullptr;
       }
+    (void)hipDeviceSynchronize();
   }
   for (auto &p : ctx->pipe)
     if (p) (void)hipStreamSynchronize(p);
@@ -694,8 +746,12 @@ int storb_rs_ctx_stats(const storb_rs_ctx *ctx, storb_rs_ctx_stats_t *out) {
   out->stream_fallbacks = ctx->n_stream_fallbacks.load();
   out->sliced_calls = ctx->n_sliced.load();
   storb_rs_ctx *c = const_cast<storb_rs_ctx *>(ctx);
-  std::lock_guard<std::mutex> lk(c->async_mu);
-  out->live_ops = c->live_ops.size();
+  {
+    std::lock_guard<std::mutex> lk(c->async_mu);
+    out->live_ops = c->live_ops.size();
+  }
+  // the table cache changes under ctx->mu (every call that launches holds it)
+  std::lock_guard<std::mutex> lk(c->mu);
   out->tables = ctx->tables.size();
   return STORB_RS_OK;
 }

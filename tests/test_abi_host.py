@@ -112,6 +112,32 @@ def test_device_numa_node_without_a_device():
     assert _lib.lib().storb_rs_device_numa_node(7) == -1
 
 
+def test_select_device_numa_topologies():
+    """storb_rs_ctx_create(-1)'s device choice, on injected
+    topologies with no device access: a thread's contexts go round-robin over
+    the GPUs on its own socket, and over all GPUs when its socket has none or
+    its node is unknown (upload.rs:418-420 through lib.rs:97-114)."""
+    sel = _lib.select_device
+    two_by_four = [0, 0, 0, 0, 1, 1, 1, 1]  # 2 sockets x 4 GPUs (an MI355X node)
+    assert [sel(0, two_by_four, t) for t in range(9)] == [0, 1, 2, 3, 0, 1, 2, 3, 0]
+    assert [sel(1, two_by_four, t) for t in range(5)] == [4, 5, 6, 7, 4]
+    interleaved = [1, 0, 1, 0, 1, 0, 1, 0]
+    assert [sel(0, interleaved, t) for t in range(4)] == [1, 3, 5, 7]
+    assert [sel(1, interleaved, t) for t in range(4)] == [0, 2, 4, 6]
+    # caller node unknown, or a node with no GPU: every GPU, plain round-robin
+    assert [sel(-1, two_by_four, t) for t in range(9)] == list(range(8)) + [0]
+    assert [sel(2, two_by_four, t) for t in range(8)] == list(range(8))
+    # devices whose node is unknown (-1) are reachable only through the fallback
+    assert [sel(0, [-1, 0, -1], t) for t in range(3)] == [1, 1, 1]
+    assert [sel(-1, [-1, 0, -1], t) for t in range(3)] == [0, 1, 2]
+    assert sel(0, [], 0) == -1
+    # every GPU of the caller's socket gets an equal share of its contexts
+    counts = [0] * 8
+    for t in range(4000):
+        counts[sel(1, two_by_four, t)] += 1
+    assert counts == [0, 0, 0, 0, 1000, 1000, 1000, 1000]
+
+
 def test_jit_compiles_decode_kernels_without_gpu():
     """The run-time-compiled decode kernels build with hipRTC on the host
     (no GPU): RS(16,8) with every data share lost, in place and assembled,
