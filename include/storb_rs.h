@@ -323,8 +323,18 @@ typedef struct {
   double compile_ms;  /* total compile wall time */
   uint64_t evicted;   /* kernels unloaded to make room (LRU, idle ones only) */
   uint64_t loaded;    /* kernels currently cached (<= STORB_RS_JIT_MAX) */
+  uint64_t refused;   /* compiled, but refused before loading: the code object
+                       * makes a function call (storb_rs_code_object_calls);
+                       * counted in `failed` too, so those matrices use the
+                       * table kernel */
 } storb_rs_jit_stats_t;
 int storb_rs_jit_stats(storb_rs_jit_stats_t *out);
+/* Whether a gfx950 code object (a raw ELF, as hipRTC returns it) has a kernel
+ * that makes a function call: 1 (why[] names it), 0 none, -1 unreadable. The
+ * library runs it on every run-time compiled kernel before loading it; an
+ * out-of-line call is how a round-4 decode kernel hung.
+ * Needs no device. */
+int storb_rs_code_object_calls(const void *code, size_t len, char *why, size_t why_len);
 /* Block until no compile is pending (benchmarks and tests). */
 int storb_rs_jit_wait(void);
 /* Ahead of the calls: queue (wait != 0: finish) the compile of the decode

@@ -54,7 +54,7 @@ class JitStats(C.Structure):
     """storb_rs_jit_stats_t (include/storb_rs.h)."""
     _fields_ = [("compiled", C.c_uint64), ("failed", C.c_uint64), ("pending", C.c_uint64),
                 ("launches", C.c_uint64), ("fallbacks", C.c_uint64), ("compile_ms", C.c_double),
-                ("evicted", C.c_uint64), ("loaded", C.c_uint64)]
+                ("evicted", C.c_uint64), ("loaded", C.c_uint64), ("refused", C.c_uint64)]
 
 
 class CtxStats(C.Structure):
@@ -143,6 +143,7 @@ def _declare(L):
     L.storb_rs_set_kernel.argtypes = [vp, C.c_int]
     L.storb_rs_sync.argtypes = [vp]
     L.storb_rs_jit_stats.argtypes = [C.POINTER(JitStats)]
+    L.storb_rs_code_object_calls.argtypes = [vp, sz, C.c_char_p, sz]
     L.storb_rs_jit_wait.argtypes = []
     L.storb_rs_jit_prepare_decode.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),
                                               C.c_uint32, C.c_int, C.c_int]
@@ -245,6 +246,14 @@ def jit_stats() -> dict:
     if rc != OK:
         raise StorbRsError(rc, "storb_rs_jit_stats")
     return {f: getattr(st, f) for f, _ in JitStats._fields_}
+
+
+def code_object_calls(code: bytes) -> tuple[int, str]:
+    """storb_rs_code_object_calls: (1 call / 0 none / -1 unreadable, why)."""
+    why = C.create_string_buffer(512)
+    buf = C.create_string_buffer(bytes(code), len(code))
+    r = lib().storb_rs_code_object_calls(buf, len(code), why, 512)
+    return r, why.value.decode()
 
 
 def jit_wait():

@@ -75,6 +75,16 @@ const char *dump_dir() {
   return d && *d ? d : nullptr;
 }
 
+// STORB_RS_JIT_TEST_CALL=1: every generated kernel gets an out-of-line call
+// (tests/test_abi_host.py checks that the compile thread refuses it).
+bool test_call() {
+  static const bool v = [] {
+    const char *e = std::getenv("STORB_RS_JIT_TEST_CALL");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 size_t max_kernels() {
   static const size_t v = [] {
     const char *e = std::getenv("STORB_RS_JIT_MAX");
@@ -231,6 +241,7 @@ class Jit {
     s->compile_ms = compile_ms_;
     s->evicted = evicted_;
     s->loaded = entries_.size();
+    s->refused = refused_;
   }
 
   std::atomic<uint64_t> launches{0}, fallbacks{0};
@@ -279,8 +290,20 @@ class Jit {
       const auto t0 = std::chrono::steady_clock::now();
       std::vector<char> code;
       std::string log;
-      const bool ok = compile(e->src, e->opt, code, log);
+      bool ok = compile(e->src, e->opt, code, log);
       register_exit_hook();
+      // Never load a kernel that makes a function call (code_object_check.cpp:
+      // the round-4 hang was an out-of-line callee that lost its return
+      // address); its matrix keeps the table kernel.
+      bool refused = false;
+      if (ok) {
+        std::string why;
+        if (code_object_calls(code.data(), code.size(), why) != 0) {
+          ok = false;
+          refused = true;
+          log = "refused: " + why;
+        }
+      }
       const double ms =
           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       {
@@ -289,9 +312,11 @@ class Jit {
         e->log = std::move(log);
         e->state = ok ? Entry::Ready : Entry::Failed;
         (ok ? compiled_ : failed_)++;
+        if (refused) refused_++;
         compile_ms_ += ms;
         pending_--;
       }
+      if (refused) std::fprintf(stderr, "storb_rs jit: %s\n", e->log.c_str());
       if (const char *dir = dump_dir()) {  // inspect with hipcc -S
         if (!ok) std::fprintf(stderr, "storb_rs jit: compile failed:\n%s\n", e->log.c_str());
         const std::string path = std::string(dir) + "/storb_bs_jit_" +
@@ -301,7 +326,7 @@ class Jit {
           std::fclose(f);
         }
         // the code object too (llvm-readelf --notes: .vgpr_count, .sgpr_count)
-        if (ok)
+        if (ok || refused)
           if (FILE *f = std::fopen((path + ".co").c_str(), "wb")) {
             std::fwrite(e->code.data(), 1, e->code.size(), f);
             std::fclose(f);
@@ -356,7 +381,7 @@ class Jit {
   std::condition_variable cv_;
   std::map<std::string, std::shared_ptr<Entry>> entries_;
   std::unordered_map<std::string, uint32_t> seen_;  // asked-for counts of keys not compiled
-  uint64_t tick_ = 0, evicted_ = 0;
+  uint64_t tick_ = 0, evicted_ = 0, refused_ = 0;
   std::deque<std::shared_ptr<Entry>> queue_;
   std::thread worker_;
   bool stop_ = false;
@@ -453,11 +478,18 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
     s += '}';
   }
   s += "}};\n};\n}  // namespace\n";
+  if (test_call()) {
+    // STORB_RS_JIT_TEST_CALL=1 (tests only): a body with an out-of-line call,
+    // which code_object_calls must refuse before anything loads it.
+    s += "__attribute__((noinline)) __device__ void storb_jit_test_callee(const storb_rs::ApplyArgs &a) {\n"
+         "  if (a.k == 0xFFFFu) reinterpret_cast<unsigned *>(a.out[0])[threadIdx.x] = 1u;\n}\n";
+  }
   // 2 waves per SIMD (<= 256 registers): without the hint, 64- and 128-lane
   // workgroups let the allocator take 257 at k = 32 (1 wave per SIMD)
   s += "extern \"C\" __global__ __launch_bounds__(" + std::to_string(sh.threads) +
        ") __attribute__((amdgpu_waves_per_eu(2))) void " + kernel_name(k, rows, copy_mask) +
        "(const storb_rs::ApplyArgs a) {\n";
+  if (test_call()) s += "  storb_jit_test_callee(a);\n";
   if (lds >= 4 && dynamic_lds(lds) == 0) {
     // Static LDS reserving 160 KiB / cap per workgroup (occupancy cap).
     s += "  __shared__ unsigned occ_pad[" + std::to_string(lds / 4) + "];\n";

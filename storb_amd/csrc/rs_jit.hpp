@@ -8,7 +8,13 @@
 
 #include "rs_args.h"
 
+#include <string>
+
 namespace storb_rs {
+// code_object_check.cpp: 1 if a kernel of the gfx950 code object makes a
+// function call (why names it), 0 if none, -1 if unreadable.
+int code_object_calls(const void *co, size_t len, std::string &why);
+
 namespace jit {
 
 // Rows one compiled matrix may have: split into launches of <= kSlotR rows

@@ -211,3 +211,92 @@ def test_device_kernels_make_no_function_calls(tmp_path):
         dis = subprocess.run([llvm, "-d", "--mcpu=gfx950", o], capture_output=True, text=True,
                              check=True).stdout
         assert "s_swappc" not in dis, os.path.basename(o)
+    # the library's own check agrees on every AOT code object
+    for o in objs:
+        r, why = _lib.code_object_calls(open(o, "rb").read())
+        assert r == 0, (os.path.basename(o), why)
+
+
+def _elf_symbols(b):
+    """(file offset of the Elf64_Sym, name, type, size) of every .symtab entry."""
+    import struct
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQII", b, shoff + i * shentsize) for i in range(shnum)]
+    out = []
+    for name, typ, _fl, _addr, off, size, link, _info in secs:
+        if typ != 2:
+            continue
+        stroff = secs[link][4]
+        for o in range(off + 24, off + size, 24):
+            nm, info, _other, _shndx, _val, sz = struct.unpack_from("<IBBHQQ", b, o)
+            end = b.index(b"\0", stroff + nm)
+            out.append((o, b[stroff + nm:end].decode(), info & 0xF, sz))
+    return out
+
+
+def _jit_subprocess(code, tmp_path, **env):
+    import sys
+    e = dict(os.environ, PYTHONPATH=ROOT, STORB_RS_JIT_DUMP=str(tmp_path), **env)
+    r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+    return json.loads(r.stdout.strip().splitlines()[-1]), r.stderr
+
+
+def test_jit_refuses_kernels_that_call(tmp_path):
+    """a run-time compiled kernel that makes a function call
+    is refused before anything loads it (the round-4 hang was such a call,
+    DESIGN.md §7). STORB_RS_JIT_TEST_CALL=1 gives every generated body an
+    out-of-line callee: the compile thread refuses it, counts it, and the
+    pattern keeps the table kernel (prepare reports the failure)."""
+    import glob
+    stats, err = _jit_subprocess(
+        "import json\n"
+        "from storb_amd import _lib\n"
+        "try:\n"
+        "    _lib.jit_prepare_decode(16, 24, list(range(8, 24)))\n"
+        "except _lib.StorbRsError:\n"
+        "    pass\n"
+        "print(json.dumps(_lib.jit_stats()))\n", tmp_path, STORB_RS_JIT_TEST_CALL="1")
+    assert stats["refused"] == 1 and stats["failed"] == 1 and stats["compiled"] == 0, stats
+    assert "refused: out-of-line function" in err
+    cos = glob.glob(str(tmp_path / "*.co"))
+    assert len(cos) == 1
+    b = bytearray(open(cos[0], "rb").read())
+    r, why = _lib.code_object_calls(bytes(b))
+    assert r == 1 and "storb_jit_test_callee" in why, why
+    # Hide the callee's body from the symbol check (size 0): the disassembly
+    # of the kernel still finds the call instruction itself.
+    import struct
+    callee = [s for s in _elf_symbols(b) if "storb_jit_test_callee" in s[1] and s[2] == 2]
+    assert callee
+    for off, _n, _t, _sz in callee:
+        struct.pack_into("<Q", b, off + 16, 0)
+    r, why = _lib.code_object_calls(bytes(b))
+    assert r == 1 and "s_swappc" in why, why
+    # not an ELF at all
+    assert _lib.code_object_calls(b"\x00" * 128)[0] == -1
+
+
+def test_jit_largest_kernels_make_no_calls(tmp_path):
+    """The shipped JIT bodies at their largest: k = 64 with
+    32 lost rows (one row-split launch) and with 2, k = 32 with 16 lost, k = 16
+    with 8 lost assembled. All compile, none is refused, and every dumped code
+    object passes the library's call check."""
+    import glob
+    stats, _ = _jit_subprocess(
+        "import json\n"
+        "from storb_amd import _lib\n"
+        "_lib.jit_prepare_decode(64, 96, list(range(32, 96)))\n"
+        "_lib.jit_prepare_decode(64, 96, list(range(2, 96)))\n"
+        "_lib.jit_prepare_decode(32, 48, list(range(16, 48)))\n"
+        "_lib.jit_prepare_decode(16, 24, list(range(8, 24)), assemble=True)\n"
+        "print(json.dumps(_lib.jit_stats()))\n", tmp_path)
+    assert stats["compiled"] == 4 and stats["refused"] == 0 and stats["failed"] == 0, stats
+    cos = sorted(glob.glob(str(tmp_path / "*.co")))
+    assert len(cos) == 4
+    for c in cos:
+        r, why = _lib.code_object_calls(open(c, "rb").read())
+        assert r == 0, (c, why)
