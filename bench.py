@@ -87,6 +87,11 @@ def parse(argv=None):
                         "v_perm tables otherwise); perm / lds force a table kernel")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--settle-ms", type=float, default=40.0,
+                   help="untimed pre-roll of whole steps (at least this long) before the "
+                        "warm-up steps: the first ~3-12 ms of load after an idle GPU run "
+                        "slower while the power controller settles (DESIGN.md §5, "
+                        "'Clock transient'); 0 disables")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--no-traffic", action="store_true",
                    help="skip the live HBM-traffic passes (rocprofv3 --pmc FETCH_SIZE / "
@@ -523,6 +528,25 @@ def shim_path_rate(ctx, seconds=0.4):
     L = _lib.lib()
     res = {"what": "per-chunk storb_rs_encode / storb_rs_decode from one thread, pageable "
                    "buffers, as the zfec-rs shim calls them (lib.rs:142-186)"}
+    # The calling thread runs on the GPU's socket, as storb_rs_ctx_create(-1)
+    # arranges on a multi-socket node (a thread gets a GPU of its own node);
+    # the numa entry below repeats the (4, 6) calls from each node.
+    gnode = L.storb_rs_device_numa_node(ctx.device)
+    by_node = _node_cpus()
+    saved = os.sched_getaffinity(0)
+    res["allowed_cpus_per_node"] = {str(k): len(v) for k, v in by_node.items()}
+    if gnode >= 0 and gnode in by_node:
+        os.sched_setaffinity(0, by_node[gnode])
+        res["caller"] = f"pinned to the {len(by_node[gnode])} allowed CPUs of NUMA node {gnode} (the GPU's)"
+    else:
+        res["caller"] = "unpinned (GPU node unknown or not in the allowed CPU set)"
+    try:
+        return _shim_rows(ctx, L, res, seconds, by_node)
+    finally:
+        os.sched_setaffinity(0, saved)
+
+
+def _shim_rows(ctx, L, res, seconds, by_node):
     cpu_ratio, xor_gbs = _contention_probe()
     res["host_probe"] = {"thread_cpu_over_wall": cpu_ratio, "numpy_xor_GBps": xor_gbs}
     rows = []
@@ -593,13 +617,40 @@ def shim_path_rate(ctx, seconds=0.4):
                          "thread_cpu_over_wall": round((time.thread_time() - c0) / wall, 3)}
         if (k, n) == (4, 6):
             row["numa"] = _shim_numa(ctx, {"encode_call": enc_call, "decode_call": dec_call},
-                                     chunk, seconds)
+                                     chunk, seconds, by_node)
         rows.append(row)
     res["geometries"] = rows
-    # Not measured here: the box's SDMA PCIe ceiling in user bytes of RS(4,2)
-    # encode (57 GB/s both directions / 1.5 bytes per user byte), cited from
-    # tools/pcie_probe.py's run, profiles/r1_pcie_probe.jsonl.
-    res["cited_sdma_ceiling_GiBps_user"] = {"value": 35.5, "source": "profiles/r1_pcie_probe.jsonl"}
+    return res
+
+
+def pcie_ceiling(dev, nbytes=256 << 20, reps=4):
+    """The box's PCIe copy rates, measured in this run (SDMA, page-locked
+    host memory): H2D, D2H and both directions at once on two streams; and
+    what that allows an RS(4,2) encode that moves 1.5 bytes per user byte
+    (data in, parity out)."""
+    h_in = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h_out = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d_in = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    res = {}
+    for name, ops in (("h2d", ((s1, d_in, h_in),)), ("d2h", ((s1, h_out, d_out),)),
+                      ("both", ((s1, d_in, h_in), (s2, h_out, d_out)))):
+        for st, dst, src in ops:  # warm
+            with torch.cuda.stream(st):
+                dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for st, dst, src in ops:
+                with torch.cuda.stream(st):
+                    dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        res[name + "_GBps"] = round(len(ops) * reps * nbytes / (time.perf_counter() - t0) / 1e9, 1)
+    res["rs42_encode_ceiling_GiBps_user"] = round(res["both_GBps"] * 1e9 / 1.5 / GIB, 2)
+    res["what"] = (f"torch pinned copies, {nbytes >> 20} MiB x {reps}, SDMA; both = H2D and D2H "
+                   f"at once on two streams; the RS(4,2) ceiling = both / 1.5 bytes moved per user "
+                   f"byte (zero-copy kernels can exceed it: they overlap the two directions)")
     return res
 
 
@@ -612,7 +663,7 @@ def _node_cpus():
     return out
 
 
-def _shim_numa(ctx, calls, chunk, seconds):
+def _shim_numa(ctx, calls, chunk, seconds, by_node):
     """The same single calls with the calling thread pinned to the CPUs of the
     GPU's NUMA node, then to those of another node of the allowed set: a
     pageable call's host copies cross the socket link when the caller sits on
@@ -620,7 +671,6 @@ def _shim_numa(ctx, calls, chunk, seconds):
     import ctypes
     libc = ctypes.CDLL(None)
     gnode = _lib.lib().storb_rs_device_numa_node(ctx.device)
-    by_node = _node_cpus()
     res = {"gpu_numa_node": gnode,
            "allowed_cpus_per_node": {str(k): len(v) for k, v in by_node.items()},
            "caller_cpu_during_default_run": _cpu_where(libc.sched_getcpu())}
@@ -954,6 +1004,149 @@ def leg_kernel_match(a, w, leg):
     return f"rs_apply_{'lds' if a.kernel == 'lds' else 'perm'}<{kb}, {r if r <= 8 else 16},"
 
 
+def _child(a, erase_pattern, steps=3, warmup=1, settle_ms=0.0):
+    """This workload as a short child run (the program rocprofv3 starts)."""
+    child = [sys.executable, os.path.abspath(__file__), "--config", str(a.config),
+             "--steps", str(steps), "--warmup", str(warmup), "--settle-ms", str(settle_ms),
+             "--minimal", "--no-check", "--kernel", a.kernel,
+             "--objects", str(a.objects), "--erase-pattern", erase_pattern,
+             "--fail", str(a.fail)]
+    if a.chunks:
+        child += ["--chunks", str(a.chunks)]
+    if a.erase is not None:
+        child += ["--erase", str(a.erase)]
+    return child
+
+
+def kernel_trace(a, w, settle_ms):
+    """One rocprofv3 --kernel-trace --stats child run of exactly this line's
+    sequence (same steps, warm-up and settle pre-roll): the launches of the
+    timed region, identified from the end of the trace (after it come only
+    the min(K, 50) steps of the per-leg event pass), their durations, and the
+    idle time between consecutive dispatches. Says whether a step's GPU time
+    is kernel time or launch gaps."""
+    import csv
+    import glob
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return {"error": "rocprofv3 not found"}
+    t0 = time.perf_counter()
+    d = tempfile.mkdtemp(prefix="storb_kt_", dir="/tmp")
+    try:
+        cmd = ["timeout", "-s", "KILL", "150", prof, "--kernel-trace", "--stats",
+               "--output-format", "csv", "-d", d, "-o", "run", "--",
+               *_child(a, a.erase_pattern, a.steps, a.warmup, settle_ms)]
+        r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"),
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            return {"error": f"rocprofv3 --kernel-trace failed (rc {r.returncode}): "
+                             f"{r.stderr.strip()[-300:]}"}
+        rows = sorted(csv.DictReader(open(files[0])), key=lambda x: int(x["Start_Timestamp"]))
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    K, probe = a.steps, min(a.steps, 50)
+    legs, lo, hi = {}, None, None
+    subs = [leg_kernel_match(a, w, leg) for leg in w.legs]
+    for li, leg in enumerate(w.legs):
+        sub = subs[li]
+        # legs that launch the same kernel (config 2: encode and decode are
+        # both rs_apply_perm<4,2>) alternate in launch order
+        same = [i for i, x in enumerate(subs) if x == sub]
+        g, pos = len(same), same.index(li)
+        mine = [x for x in rows if sub in x["Kernel_Name"]]
+        if len(mine) < (K + probe) * g:
+            return {"error": f"{len(mine)} {sub} launches in the trace, expected >= "
+                             f"{(K + probe) * g}"}
+        timed = mine[len(mine) - (K + probe) * g:len(mine) - probe * g][pos::g]
+        dur = [(int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3 for x in timed]
+        avg = sum(dur) / len(dur)
+        legs[leg] = {"kernel": timed[0]["Kernel_Name"][:120], "launches": len(dur),
+                     "avg_us": round(avg, 2), "median_us": round(statistics.median(dur), 2),
+                     "min_us": round(min(dur), 2), "max_us": round(max(dur), 2),
+                     "first_half_avg_us": round(sum(dur[:len(dur) // 2]) / max(1, len(dur) // 2), 2),
+                     "second_half_avg_us": round(sum(dur[len(dur) // 2:]) /
+                                                 max(1, len(dur) - len(dur) // 2), 2),
+                     "durations_us": [round(x, 1) for x in dur[:64]],
+                     "frac_kernel_time": round(w.alg_bytes(leg) / (avg * 1e-6) / 1e9 /
+                                               HBM_PEAK_GBS, 4)}
+        s0, e1 = int(timed[0]["Start_Timestamp"]), int(timed[-1]["End_Timestamp"])
+        lo = s0 if lo is None else min(lo, s0)
+        hi = e1 if hi is None else max(hi, e1)
+    win = [x for x in rows if lo <= int(x["Start_Timestamp"]) and int(x["End_Timestamp"]) <= hi]
+    gaps = [(int(win[i + 1]["Start_Timestamp"]) - int(win[i]["End_Timestamp"])) / 1e3
+            for i in range(len(win) - 1)]
+    busy = sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in win) / 1e6
+    span = (hi - lo) / 1e6
+    return {"legs": legs, "dispatches_in_window": len(win),
+            "window_ms_per_step": round(span / K, 4), "busy_ms_per_step": round(busy / K, 4),
+            "idle_ms_per_step": round((span - busy) / K, 4),
+            "median_gap_us": round(statistics.median(gaps), 2) if gaps else None,
+            "max_gap_us": round(max(gaps), 2) if gaps else None,
+            "settle_ms": settle_ms,
+            "source": (f"rocprofv3 --kernel-trace --stats over a child run with this line's "
+                       f"--steps {K} --warmup {a.warmup} --settle-ms {settle_ms} "
+                       f"({time.perf_counter() - t0:.0f} s); the timed launches are the {K} "
+                       f"per leg before the last {probe} (the per-leg event pass); the "
+                       f"tracer itself adds ~2-3 us to each gap")}
+
+
+def settle_device(legs, stream, ms):
+    """Run whole steps, untimed, for at least `ms` of wall time. After an
+    idle period the chip comes up at full clock and its power controller
+    then pulls back: in the kernel traces (profiles/r5a_*) launches 3-12 ms
+    into the load take 250-268 us against 238-242 us before and after, so a
+    10 ms timed region that starts 4 ms after the load began (the driver's
+    --steps 20 --warmup 5) measured that transient, not the kernel."""
+    if ms <= 0:
+        return {"ms": 0.0, "steps": 0}
+    t0, n = time.perf_counter(), 0
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(8):
+            for f in legs:
+                f()
+        n += 8
+        stream.synchronize()
+    return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "steps": n}
+
+
+def gpu_clocks(local):
+    """The GPU's clock levels and power cap (sysfs of this device's PCI
+    function; amd-smi reports the same values): current gfx / memory / fabric
+    levels (the '*' entry of pp_dpm_*) and power1_cap / power1_average in W."""
+    import glob
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(32)
+        if hip.hipDeviceGetPCIBusId(buf, 32, local) != 0:
+            return {"error": "hipDeviceGetPCIBusId failed"}
+        base = "/sys/bus/pci/devices/" + buf.value.decode().lower()
+    except OSError as e:
+        return {"error": repr(e)}
+    out = {"pci": base.rsplit("/", 1)[-1]}
+    for name in ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk", "pp_dpm_socclk",
+                 "power_dpm_force_performance_level"):
+        try:
+            txt = open(os.path.join(base, name)).read().strip().splitlines()
+        except OSError:
+            continue
+        cur = [x for x in txt if x.rstrip().endswith("*")]
+        out[name] = (cur[0].split(":", 1)[1].strip(" *") if cur else txt[0].strip())
+    for name in ("power1_cap", "power1_average", "power1_input"):
+        for f in glob.glob(os.path.join(base, "hwmon", "hwmon*", name)):
+            try:
+                out[name + "_W"] = round(int(open(f).read()) / 1e6, 1)
+            except (OSError, ValueError):
+                pass
+    return out
+
+
 def _pmc_passes(a, erase_pattern, seq=False):
     """Two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child
     run of this workload: ({(kernel name, counter): [values in launch
@@ -967,14 +1160,7 @@ def _pmc_passes(a, erase_pattern, seq=False):
     prof = shutil.which("rocprofv3")
     if not prof:
         return None, "rocprofv3 not found"
-    child = [sys.executable, os.path.abspath(__file__), "--config", str(a.config),
-             "--steps", "3", "--warmup", "1", "--minimal", "--no-check", "--kernel", a.kernel,
-             "--objects", str(a.objects), "--erase-pattern", erase_pattern,
-             "--fail", str(a.fail)]
-    if a.chunks:
-        child += ["--chunks", str(a.chunks)]
-    if a.erase is not None:
-        child += ["--erase", str(a.erase)]
+    child = _child(a, erase_pattern)
     env = dict(os.environ, TMPDIR="/tmp")
     vals = {}
     for cnt in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -1273,7 +1459,7 @@ def line_extras(rank, world, minimal, config):
     ex = {"cpu_baseline"}
     if world > 1:
         return ex
-    ex |= {"traffic", "copy_ceiling"}
+    ex |= {"traffic", "copy_ceiling", "kernel_trace"}
     if config in (2, 5, 6):
         ex |= {"cpu_threads", "host_path", "shim_path", "hashing", "repair", "download"}
     if config == 3:
@@ -1368,6 +1554,8 @@ def main():
             w.jit_legs.add(leg)
     jit0 = _lib.jit_stats()
     legs = [getattr(w, leg) for leg in w.legs]
+    clocks0 = gpu_clocks(local) if rank == 0 and not a.minimal else None
+    settled = settle_device(legs, stream, a.settle_ms)
     for _ in range(a.warmup):
         for f in legs:
             f()
@@ -1400,6 +1588,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = e_start.elapsed_time(e_end) / a.steps
+    clocks1 = gpu_clocks(local) if rank == 0 and not a.minimal else None
     jit1 = _lib.jit_stats()
     if not each:
         # Per-leg split (which kernel took what) from an untimed pass of the
@@ -1464,6 +1653,8 @@ def main():
         },
         "launch": ranks,
         "per_rank": per_rank,
+        "settle": dict(settled, why="untimed whole steps before the warm-up: the power "
+                                    "controller's transient after an idle GPU (settle_device)"),
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -1495,6 +1686,20 @@ def main():
         "cpu_baseline": None,
     }
     ex = line_extras(rank, world, a.minimal, a.config)
+    if clocks0 is not None:
+        out["roofline"]["gpu_clocks"] = {"before_settle": clocks0, "after_timed_region": clocks1}
+    if "kernel_trace" in ex:
+        kt = kernel_trace(a, w, a.settle_ms)
+        if "legs" in kt:
+            # without the pre-roll: what a short region right after idle measures
+            kt0 = kernel_trace(a, w, 0.0)
+            kt["without_settle"] = ({k: kt0[k] for k in ("window_ms_per_step",
+                                                         "busy_ms_per_step", "median_gap_us")}
+                                    | {"legs": {leg: {x: v[x] for x in (
+                                        "avg_us", "first_half_avg_us", "second_half_avg_us",
+                                        "durations_us")} for leg, v in kt0["legs"].items()}}
+                                    if "legs" in kt0 else kt0)
+        out["roofline"]["kernel_trace"] = kt
     if "traffic" in ex and not a.no_traffic:
         if any(v > 1 for leg, v in out["roofline"]["launches_per_leg"].items()
                if not (leg == "decode" and w.sets is not None)):
@@ -1524,11 +1729,13 @@ def main():
             w.k, w.n, w.chunk, er, threads=nproc, nchunks=max(nch, nproc))
         out["cpu_baseline_nproc"]["cpu_quota"] = cpu_quota()
     if "host_path" in ex and not a.no_host_path:
+        pc = pcie_ceiling(dev)
         out["pcie_inclusive"] = host_path_rate(ctx, w.k, w.n, w.chunk,
                                                nchunks=max(8, (256 << 20) // w.chunk),
                                                erased=[e for e in w.fixed_erased if e < w.k],
                                                sets=w.sets or download_sets(
                                                    w.k, w.n, 64, SEED_BASE + 4343))
+        out["pcie_inclusive"]["pcie_ceiling"] = pc
     if "shim_path" in ex:
         out["shim_path"] = shim_path_rate(ctx)
     if "hashing" in ex:

@@ -24,11 +24,11 @@ namespace {
 constexpr int kB3Threads = 256;
 typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
 
-// One out-of-line copy of the 7-round compression (~700 instructions): the
-// chunk, parent and root paths all call it, so the kernel's code stays
-// inside the instruction cache (inlined it was ~6k instructions).
-// Arguments are scalars and the result a small struct so the call passes
-// everything in VGPRs (array pointers would force the arrays to scratch).
+// The 7-round compression behind one scalar-argument interface, so the
+// chunk, parent and root paths share a call shape whose arguments and result
+// stay in VGPRs (array pointers would force the arrays to scratch). It is
+// inlined like every device function of the library: the kernels make no
+// calls (code_object_check.cpp, tests/test_abi_host.py).
 struct CV8 {
   uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
 };
@@ -175,9 +175,19 @@ __device__ __forceinline__ void store_hash(uint8_t *o, const uint32_t *cv) {
     for (int b = 0; b < 4; b++) o[4 * w + b] = static_cast<uint8_t>(cv[w] >> (8 * b));
 }
 
+// Shard i of a launch is share t = i % per of stripe s = i / per: shares
+// t < k at in0 + s * stride0 + t * pitch (data shares of a chunk, back to
+// back), the rest at in1 + s * stride1 + (t - k) * pitch (its parity);
+// digest at out + i * 32, i.e. [stripe][share]. A plain batch is per = k = 1.
+struct B3Map {
+  const uint8_t *in0, *in1;
+  uint64_t stride0, stride1, pitch;
+  uint32_t per, k;
+};
+
 __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
-    const uint8_t *in, uint64_t len, uint64_t stride, uint8_t *out, uint32_t count,
-    uint32_t q_log2, uint32_t depth, uint32_t seg_log2) {
+    const B3Map mp, uint64_t len, uint8_t *out, uint32_t count, uint32_t q_log2, uint32_t depth,
+    uint32_t seg_log2) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds3[];
   // A segment of L = 2^seg_log2 lanes hashes one shard; a workgroup holds
   // T / L segments (small shards pack several to a workgroup, large ones
@@ -192,7 +202,9 @@ __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
   // Segments past the last shard redo the last one (every lane must reach
   // the barriers below) and store nothing.
   const uint32_t shard = live ? shard_raw : count - 1;
-  const uint8_t *p = in + static_cast<uint64_t>(shard) * stride;
+  const uint32_t st = shard / mp.per, t = shard - st * mp.per;
+  const uint8_t *p = t < mp.k ? mp.in0 + st * mp.stride0 + static_cast<uint64_t>(t) * mp.pitch
+                              : mp.in1 + st * mp.stride1 + static_cast<uint64_t>(t - mp.k) * mp.pitch;
   uint8_t *o = out + static_cast<uint64_t>(shard) * 32;
   const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(p)) & 15) == 0;
@@ -281,8 +293,8 @@ __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
 // Largest message the LDS tree handles: 256 lanes x 64 chunks = 16 MiB.
 constexpr uint64_t kB3MaxLen = 256ull * 64 * b3::kChunkLen;
 
-hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
-                               uint64_t stride, uint8_t *out, hipStream_t s) {
+static hipError_t launch_b3(const B3Map &mp, uint64_t len, uint32_t count, uint8_t *out,
+                            hipStream_t s) {
   if (count == 0) return hipSuccess;
   if (len > kB3MaxLen) return hipErrorInvalidValue;
   const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
@@ -303,9 +315,23 @@ hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
   const size_t lds = n == 1 ? 0 : (static_cast<size_t>(depth) + 2) * 8 * T * sizeof(uint32_t);
   const uint32_t per_block = static_cast<uint32_t>(T) / L;
   const uint32_t blocks = (count + per_block - 1) / per_block;
-  hipLaunchKernelGGL(blake3_batch_kernel, dim3(blocks), dim3(T), lds, s, in, len, stride, out,
-                     count, q_log2, depth, seg_log2);
+  hipLaunchKernelGGL(blake3_batch_kernel, dim3(blocks), dim3(T), lds, s, mp, len, out, count,
+                     q_log2, depth, seg_log2);
   return hipGetLastError();
+}
+
+hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
+                               uint64_t stride, uint8_t *out, hipStream_t s) {
+  return launch_b3(B3Map{in, in, stride, stride, 0, 1, 1}, len, count, out, s);
+}
+
+hipError_t launch_blake3_stripes(const uint8_t *data, uint64_t data_stride, const uint8_t *parity,
+                                 uint64_t parity_stride, uint64_t pitch, uint32_t k, uint32_t n,
+                                 uint64_t len, uint32_t nstripes, uint8_t *out, hipStream_t s) {
+  if (n == 0 || k > n || static_cast<uint64_t>(nstripes) * n > 0xFFFFFFFFull)
+    return hipErrorInvalidValue;
+  return launch_b3(B3Map{data, parity, data_stride, parity_stride, pitch, n, k}, len,
+                   nstripes * n, out, s);
 }
 
 }  // namespace storb_rs

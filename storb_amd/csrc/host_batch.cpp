@@ -69,9 +69,9 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   }
   const uint32_t nb = (nchunks + batch - 1) / batch;
   HostPool &pool = host_pool(ctx);
-  // Whether batch buffer b's digests came from the fused kernel (its [c][t]
-  // layout) or from the two hash launches ([c][j] data, then [c][i] parity):
-  // try_encode_hash may decline a batch the up-front check let through.
+  // Whether batch buffer b's digests came from the fused kernel or need the
+  // hash launch: try_encode_hash may decline a batch the up-front check let
+  // through.
   bool did_fuse[2] = {false, false};
   auto unpack = [&](uint32_t bi) {
     const int b = bi & 1;
@@ -88,21 +88,10 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
         });
       }
     }
-    if (hashes_out && did_fuse[b]) {
+    if (hashes_out)  // [c][t] from either the fused kernel or the hash launch
       std::memcpy(hashes_out + static_cast<size_t>(c0) * n * 32,
                   ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch,
                   static_cast<size_t>(cn) * n * 32);
-    } else if (hashes_out) {
-      // device order: [c][j] data digests, then [c][i] parity digests
-      const uint8_t *hd = ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch;
-      const uint8_t *hp = hd + static_cast<size_t>(cn) * k * 32;
-      for (uint32_t c = 0; c < cn; c++) {
-        uint8_t *o = hashes_out + (static_cast<size_t>(c0) + c) * n * 32;
-        std::memcpy(o, hd + static_cast<size_t>(c) * k * 32, static_cast<size_t>(k) * 32);
-        std::memcpy(o + static_cast<size_t>(k) * 32, hp + static_cast<size_t>(c) * p * 32,
-                    static_cast<size_t>(p) * 32);
-      }
-    }
   };
   for (uint32_t bi = 0; bi < nb; bi++) {
     const int b = bi & 1;
@@ -169,13 +158,9 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
       if (rc) return rc;
     }
     size_t back = static_cast<size_t>(p) * S * cn;
-    if (hashes_out && !did_fuse[b]) {
-      // shares are pitched S apart across the whole batch: one launch each
-      HIP_TRY(ctx, launch_blake3_batch(dd, B, cn * k, S, dh, s));
-      if (p > 0)
-        HIP_TRY(ctx, launch_blake3_batch(dp, B, cn * p, S, dh + static_cast<size_t>(cn) * k * 32,
-                                         s));
-    }
+    if (hashes_out && !did_fuse[b])  // every share of the batch, one launch, [c][t] digests
+      HIP_TRY(ctx, launch_blake3_stripes(dd, per, dp, static_cast<size_t>(p) * S, S, k, n, B, cn,
+                                         dh, s));
     if (back)
       HIP_TRY(ctx, hipMemcpyAsync(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
                                              : ctx->pipe_out[b].p,

@@ -98,6 +98,13 @@ hipError_t launch_encode_bitslice_stream(const ApplyArgs &a, uint32_t n, const S
 
 hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
                                uint64_t stride, uint8_t *out, hipStream_t s);
+// Every share of nstripes stripes in one launch: len bytes of data share t <
+// k of stripe s at data + s * data_stride + t * pitch, of parity share t >= k
+// at parity + s * parity_stride + (t - k) * pitch; digest of (s, t) at out +
+// (s * n + t) * 32.
+hipError_t launch_blake3_stripes(const uint8_t *data, uint64_t data_stride, const uint8_t *parity,
+                                 uint64_t parity_stride, uint64_t pitch, uint32_t k, uint32_t n,
+                                 uint64_t len, uint32_t nstripes, uint8_t *out, hipStream_t s);
 
 // Encode with the blake3 digest of every share in the same pass
 // (rs_encode_hash.hip). Stripe s: data share j at data + s*data_stride +

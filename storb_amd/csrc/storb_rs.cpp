@@ -651,6 +651,14 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   if (const char *e = std::getenv("STORB_RS_ZC_MAX")) c->zc_max = std::strtoull(e, nullptr, 10);
   if (const char *e = std::getenv("STORB_RS_ZC_BATCH")) c->zc_batch = std::atoi(e) != 0;
   if (const char *e = std::getenv("STORB_RS_FUSED_HASH")) c->fused_hash = std::atoi(e) != 0;
+  if (const char *e = std::getenv("STORB_RS_EH_SUB")) {
+    unsigned sub = 0;
+    int mode = 0;
+    if (std::sscanf(e, "%u,%d", &sub, &mode) >= 1) {
+      c->eh_sub = sub;
+      c->eh_mode = mode;
+    }
+  }
   if (const char *e = std::getenv("STORB_RS_TABLE_CACHE"))
     c->table_cap = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
   if (const char *e = std::getenv("STORB_RS_TEST_STREAM_STALL")) {
@@ -704,6 +712,11 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->eh_stream) {
+    (void)hipStreamSynchronize(ctx->eh_stream);
+    (void)hipStreamDestroy(ctx->eh_stream);
+  }
+  for (auto &e : ctx->eh_ev) (void)hipEventDestroy(e);
   if (ctx->desc_stream) {
     (void)hipStreamSynchronize(ctx->desc_stream);
     (void)hipStreamDestroy(ctx->desc_stream);
@@ -1077,6 +1090,55 @@ bool try_encode_hash(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
 
 extern "C" {
 
+// Sub-batches of ctx->eh_sub stripes: encode sub-batch i on s, then its
+// hash -- on ctx->eh_stream after an event (mode 0: the hash of i runs while
+// s encodes i + 1), or on s itself (mode 1: no concurrency, but each hash
+// reads shares the encode touched a moment before). s ends after every hash.
+static int encode_hash_pipelined(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
+                                 uint32_t nstripes, const uint8_t *d_data, size_t data_stride,
+                                 uint8_t *d_parity, size_t parity_stride, uint8_t *d_hashes,
+                                 hipStream_t s) {
+  const uint32_t p = n - k, sub = ctx->eh_sub;
+  const uint32_t nb = (nstripes + sub - 1) / sub;
+  const bool two = ctx->eh_mode == 0;
+  if (two && !ctx->eh_stream)
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->eh_stream, hipStreamNonBlocking));
+  while (ctx->eh_ev.size() < nb + 1) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(ctx, hipEventCreateWithFlags(&e, kOrderEvent));
+    ctx->eh_ev.push_back(e);
+  }
+  hipStream_t hs = two ? ctx->eh_stream : s;
+  if (two) {  // the hash stream starts after everything queued on s so far
+    HIP_TRY(ctx, hipEventRecord(ctx->eh_ev[nb], s));
+    HIP_TRY(ctx, hipStreamWaitEvent(hs, ctx->eh_ev[nb], 0));
+  }
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t s0 = b * sub, cnt = std::min(sub, nstripes - s0);
+    const uint8_t *dd = d_data + static_cast<size_t>(s0) * data_stride;
+    uint8_t *dp = d_parity + static_cast<size_t>(s0) * parity_stride;
+    std::vector<const uint8_t *> in(k);
+    std::vector<size_t> ins(k, data_stride), outs(p, parity_stride);
+    std::vector<uint8_t *> out(p);
+    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * block;
+    for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * block;
+    const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), block,
+                                cnt, s);
+    if (rc) return rc;
+    if (two) {
+      HIP_TRY(ctx, hipEventRecord(ctx->eh_ev[b], s));
+      HIP_TRY(ctx, hipStreamWaitEvent(hs, ctx->eh_ev[b], 0));
+    }
+    HIP_TRY(ctx, launch_blake3_stripes(dd, data_stride, dp, parity_stride, block, k, n, block,
+                                       cnt, d_hashes + static_cast<size_t>(s0) * n * 32, hs));
+  }
+  if (two) {
+    HIP_TRY(ctx, hipEventRecord(ctx->eh_ev[nb], hs));
+    HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->eh_ev[nb], 0));
+  }
+  return STORB_RS_OK;
+}
+
 int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
                                uint32_t nstripes, const uint8_t *d_data, size_t data_stride,
                                uint8_t *d_parity, size_t parity_stride, uint8_t *d_hashes,
@@ -1099,9 +1161,12 @@ int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t
     HIP_TRY(ctx, e);
     return STORB_RS_OK;
   }
-  // Two kernels: encode, then one hash launch per share slot into a
-  // stream-ordered scratch, scattered to (s*n + t)*32.
+  // Two kernels: encode, then one hash launch over all n shares of every
+  // stripe (digests written at (s*n + t)*32 directly).
   const uint32_t p = n - k;
+  if (p > 0 && ctx->eh_sub > 0 && nstripes > ctx->eh_sub)
+    return encode_hash_pipelined(ctx, k, n, block, nstripes, d_data, data_stride, d_parity,
+                                 parity_stride, d_hashes, s);
   if (p > 0) {
     std::vector<const uint8_t *> in(k);
     std::vector<size_t> ins(k, data_stride), outs(p, parity_stride);
@@ -1112,22 +1177,9 @@ int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t
                                 nstripes, s);
     if (rc) return rc;
   }
-  uint8_t *tmp = nullptr;
-  const size_t per = static_cast<size_t>(nstripes) * 32;
-  HIP_TRY(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), per * n, s));
-  hipError_t err = hipSuccess;
-  for (uint32_t t = 0; t < n && err == hipSuccess; t++) {
-    const uint8_t *base = t < k ? d_data + static_cast<size_t>(t) * block
-                                : d_parity + static_cast<size_t>(t - k) * block;
-    err = launch_blake3_batch(base, block, nstripes, t < k ? data_stride : parity_stride,
-                              tmp + t * per, s);
-    if (err == hipSuccess)
-      err = hipMemcpy2DAsync(d_hashes + static_cast<size_t>(t) * 32, static_cast<size_t>(n) * 32,
-                             tmp + t * per, 32, 32, nstripes, hipMemcpyDeviceToDevice, s);
-  }
-  const hipError_t ef = hipFreeAsync(tmp, s);
-  HIP_TRY(ctx, err);
-  HIP_TRY(ctx, ef);
+  // every share of every stripe in one hash launch, digests in place
+  HIP_TRY(ctx, launch_blake3_stripes(d_data, data_stride, d_parity, parity_stride, block, k, n,
+                                     block, nstripes, d_hashes, s));
   return STORB_RS_OK;
 }
 
