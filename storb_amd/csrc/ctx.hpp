@@ -216,15 +216,6 @@ struct storb_rs_ctx {
   // Encode + blake3 piece ids in one kernel (rs_encode_hash.hip) where the
   // geometry has one; 0 = encode kernel then hash kernel. STORB_RS_FUSED_HASH.
   bool fused_hash = true;
-  // Encode + piece ids for geometries without a fused kernel: sub-batches of
-  // eh_sub stripes, encode i + 1 on the call's stream while the hash of i
-  // runs on eh_stream (eh_mode 0), or both on the call's stream interleaved
-  // (eh_mode 1). 0 = encode everything, then hash everything.
-  // STORB_RS_EH_SUB="<stripes>[,<mode>]" (A/B).
-  uint32_t eh_sub = 0;
-  int eh_mode = 0;
-  hipStream_t eh_stream = nullptr;
-  std::vector<hipEvent_t> eh_ev;
   hipEvent_t slice_ev[storb_rs::detail::kMaxSlices] = {};  // sliced single-call pipeline
   // Slice-completion words the single-call streams write (64 B apart) and
   // the host spins on (host_calls.cpp slice_signal / slice_wait).

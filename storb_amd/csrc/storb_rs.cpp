@@ -651,14 +651,6 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   if (const char *e = std::getenv("STORB_RS_ZC_MAX")) c->zc_max = std::strtoull(e, nullptr, 10);
   if (const char *e = std::getenv("STORB_RS_ZC_BATCH")) c->zc_batch = std::atoi(e) != 0;
   if (const char *e = std::getenv("STORB_RS_FUSED_HASH")) c->fused_hash = std::atoi(e) != 0;
-  if (const char *e = std::getenv("STORB_RS_EH_SUB")) {
-    unsigned sub = 0;
-    int mode = 0;
-    if (std::sscanf(e, "%u,%d", &sub, &mode) >= 1) {
-      c->eh_sub = sub;
-      c->eh_mode = mode;
-    }
-  }
   if (const char *e = std::getenv("STORB_RS_TABLE_CACHE"))
     c->table_cap = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
   if (const char *e = std::getenv("STORB_RS_TEST_STREAM_STALL")) {
@@ -712,11 +704,6 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
-  if (ctx->eh_stream) {
-    (void)hipStreamSynchronize(ctx->eh_stream);
-    (void)hipStreamDestroy(ctx->eh_stream);
-  }
-  for (auto &e : ctx->eh_ev) (void)hipEventDestroy(e);
   if (ctx->desc_stream) {
     (void)hipStreamSynchronize(ctx->desc_stream);
     (void)hipStreamDestroy(ctx->desc_stream);
@@ -1090,55 +1077,6 @@ bool try_encode_hash(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
 
 extern "C" {
 
-// Sub-batches of ctx->eh_sub stripes: encode sub-batch i on s, then its
-// hash -- on ctx->eh_stream after an event (mode 0: the hash of i runs while
-// s encodes i + 1), or on s itself (mode 1: no concurrency, but each hash
-// reads shares the encode touched a moment before). s ends after every hash.
-static int encode_hash_pipelined(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
-                                 uint32_t nstripes, const uint8_t *d_data, size_t data_stride,
-                                 uint8_t *d_parity, size_t parity_stride, uint8_t *d_hashes,
-                                 hipStream_t s) {
-  const uint32_t p = n - k, sub = ctx->eh_sub;
-  const uint32_t nb = (nstripes + sub - 1) / sub;
-  const bool two = ctx->eh_mode == 0;
-  if (two && !ctx->eh_stream)
-    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->eh_stream, hipStreamNonBlocking));
-  while (ctx->eh_ev.size() < nb + 1) {
-    hipEvent_t e = nullptr;
-    HIP_TRY(ctx, hipEventCreateWithFlags(&e, kOrderEvent));
-    ctx->eh_ev.push_back(e);
-  }
-  hipStream_t hs = two ? ctx->eh_stream : s;
-  if (two) {  // the hash stream starts after everything queued on s so far
-    HIP_TRY(ctx, hipEventRecord(ctx->eh_ev[nb], s));
-    HIP_TRY(ctx, hipStreamWaitEvent(hs, ctx->eh_ev[nb], 0));
-  }
-  for (uint32_t b = 0; b < nb; b++) {
-    const uint32_t s0 = b * sub, cnt = std::min(sub, nstripes - s0);
-    const uint8_t *dd = d_data + static_cast<size_t>(s0) * data_stride;
-    uint8_t *dp = d_parity + static_cast<size_t>(s0) * parity_stride;
-    std::vector<const uint8_t *> in(k);
-    std::vector<size_t> ins(k, data_stride), outs(p, parity_stride);
-    std::vector<uint8_t *> out(p);
-    for (uint32_t j = 0; j < k; j++) in[j] = dd + static_cast<size_t>(j) * block;
-    for (uint32_t i = 0; i < p; i++) out[i] = dp + static_cast<size_t>(i) * block;
-    const int rc = encode_apply(ctx, k, n, in.data(), ins.data(), out.data(), outs.data(), block,
-                                cnt, s);
-    if (rc) return rc;
-    if (two) {
-      HIP_TRY(ctx, hipEventRecord(ctx->eh_ev[b], s));
-      HIP_TRY(ctx, hipStreamWaitEvent(hs, ctx->eh_ev[b], 0));
-    }
-    HIP_TRY(ctx, launch_blake3_stripes(dd, data_stride, dp, parity_stride, block, k, n, block,
-                                       cnt, d_hashes + static_cast<size_t>(s0) * n * 32, hs));
-  }
-  if (two) {
-    HIP_TRY(ctx, hipEventRecord(ctx->eh_ev[nb], hs));
-    HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->eh_ev[nb], 0));
-  }
-  return STORB_RS_OK;
-}
-
 int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block,
                                uint32_t nstripes, const uint8_t *d_data, size_t data_stride,
                                uint8_t *d_parity, size_t parity_stride, uint8_t *d_hashes,
@@ -1162,11 +1100,14 @@ int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t
     return STORB_RS_OK;
   }
   // Two kernels: encode, then one hash launch over all n shares of every
-  // stripe (digests written at (s*n + t)*32 directly).
+  // stripe (digests written at (s*n + t)*32 directly). Sub-batches pipelined
+  // over two streams (the hash of batch i beside the encode of i + 1) and
+  // interleaved on one stream both measured slower at every size, e.g.
+  // (16, 24) x 128 stripes 0.895 ms sequential vs 0.90-1.46 ms
+  // (profiles/r5d_widehash_pipelining.jsonl): a sub-batch's hash launch has
+  // too few shards to fill the chip, and the encoder's LDS reservation keeps
+  // the two kernels off each other's CUs.
   const uint32_t p = n - k;
-  if (p > 0 && ctx->eh_sub > 0 && nstripes > ctx->eh_sub)
-    return encode_hash_pipelined(ctx, k, n, block, nstripes, d_data, data_stride, d_parity,
-                                 parity_stride, d_hashes, s);
   if (p > 0) {
     std::vector<const uint8_t *> in(k);
     std::vector<size_t> ins(k, data_stride), outs(p, parity_stride);

@@ -108,6 +108,28 @@ __global__ __launch_bounds__(T) void dl_mix(const Args a) {
   }
 }
 
+// Persistent: gridDim.x workgroups (cap x CUs), each striding over the
+// launch's tiles in order, so the resident set always covers a contiguous
+// run of tiles and no workgroup is dispatched twice.
+template <int K, int T, int U>
+__global__ __launch_bounds__(T) void dl_persist(const Args a, uint32_t total) {
+  const uint32_t tiles = a.cols / (T * U);
+  for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+    const uint32_t item = g / tiles, t = g - item * tiles;
+    cu64 *q = (cu64 *)(a.rec) + static_cast<uint64_t>(item) * kRecQ;
+    const uint32_t r = static_cast<uint32_t>(q[0] >> 32);
+    const uint32_t c0 = t * T * U + threadIdx.x;
+    if (r <= 1)
+      tile<K, 1, T, U>(q, c0);
+    else if (r == 2)
+      tile<K, 2, T, U>(q, c0);
+    else if (r == 3)
+      tile<K, 3, T, U>(q, c0);
+    else
+      tile<K, 4, T, U>(q, c0);
+  }
+}
+
 // The uniform reference: contiguous stripes, addresses computed (k inputs
 // then r outputs per stripe, each B bytes), no record.
 template <int K, int R, int T>
@@ -219,6 +241,22 @@ int main(int argc, char **argv) {
                                std::to_string(tpw) + " cap=" + std::to_string(cap),
                            bytes, [=](hipStream_t st) { kern(blocks, T, dyn, st, a); }, {}});
     };
+    auto add_persist = [&](int K, int T, int per_cu) {
+      const uint32_t tiles = cols / T, total = tiles * nitems;
+      const uint32_t grid = std::min<uint32_t>(total, 256u * per_cu);
+      Args a{drec, sh.k, cols, 1};
+      const size_t dyn = cap_lds(per_cu);
+      vs.push_back(Variant{"persistent T=" + std::to_string(T) + " wg/CU=" + std::to_string(per_cu),
+                           bytes,
+                           [=](hipStream_t st) {
+                             if (K == 4)
+                               launch<dl_persist<4, 256, 1>>(grid, T, dyn, st, a, total);
+                             else
+                               launch<dl_persist<16, 256, 1>>(grid, T, dyn, st, a, total);
+                           },
+                           {}});
+    };
+    for (int pc : {2, 4, 6, 8}) add_persist(static_cast<int>(sh.k), 256, pc);
 #define MIX(K, T, U)                                                                    \
   [](uint32_t b, int t, size_t d, hipStream_t st, Args a) {                             \
     launch<dl_mix<K, T, U>>(b, t, d, st, a);                                            \

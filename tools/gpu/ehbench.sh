@@ -4,6 +4,8 @@
 # usage: tools/gpu/ehbench.sh OUTDIR
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+# tools/_build does not travel to the box (.gpurunignore): build there
+make -s -j4 -C tools ehbench > /dev/null || exit 1
 O=gpurun_out/${1:-eh}; mkdir -p $O
 timeout -k 10 240 tools/_build/ehbench 5 5 > $O/ehbench.txt 2>&1 || { cat $O/ehbench.txt; exit 1; }
 cat $O/ehbench.txt

@@ -5,6 +5,8 @@
 # usage: tools/gpu/kernel_sweeps.sh OUTDIR
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+# tools/_build does not travel to the box (.gpurunignore): build there
+make -s -j4 -C tools mixbench k32_tune descbench > /dev/null || exit 1
 O=gpurun_out/${1:-sweeps}; mkdir -p $O
 timeout -k 10 120 tools/_build/mixbench 25 16 > $O/mixbench16.txt 2>&1 && cat $O/mixbench16.txt &&
 timeout -k 10 120 tools/_build/mixbench 25 32 > $O/mixbench32.txt 2>&1 && cat $O/mixbench32.txt &&

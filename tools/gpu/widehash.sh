@@ -10,4 +10,4 @@ export TMPDIR=/tmp
 timeout -k 10 300 python tools/widehash.py > "$out/widehash.jsonl" 2> "$out/widehash.err" || exit $?
 cat "$out/widehash.jsonl"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/prof" -o run -- \
-  python3 tools/widehash.py --reps 5 --subs 16 > "$out/prof.jsonl" 2>> "$out/widehash.err" || exit $?
+  python3 tools/widehash.py --reps 5 > "$out/prof.jsonl" 2>> "$out/widehash.err" || exit $?

@@ -274,6 +274,17 @@ def _run(a, miners, inspect=None):
         "upload_GiBps": round(a.size / GIB / t_upload, 3),
         "download_GiBps": round(a.size / GIB / t_download, 3),
         "end_to_end_GiBps": round(a.size / GIB / (t_upload + t_download), 3),
+        # the two GPU legs (host in / host out, PCIe included) apart from the
+        # harness's Python socket legs, which bound the end-to-end figure
+        "gpu_legs": {"encode_with_piece_ids_GiBps": round(a.size / GIB / t_encode, 3),
+                     "batched_reconstruct_GiBps": round(a.size / GIB / t_decode, 3),
+                     "what": "objects.encode_object (storb_rs_encode_chunks_hashed) and "
+                             "objects.reconstruct_object (storb_rs_decode_chunks), host "
+                             "buffers in and out, PCIe included"},
+        "harness_legs": {"store_framing_upload_s": round(t_upload - t_encode, 4),
+                         "python_fetch_s": round(t_fetch, 4),
+                         "what": "Python sockets / HTTP of this harness (wire.py), not the "
+                                 "GPU path: the end-to-end figure is bound by these"},
         "devices": [c.device for c in ctxs], "contexts": len(ctxs), "warm": not a.cold,
         "visible_gpus": _lib.device_count(),
     }

@@ -1,14 +1,12 @@
 #!/usr/bin/env python3
 """Encode + piece ids at Storb's wide geometries: the
-device-resident storb_rs_encode_hashed_dev against encode alone and against
-encode-then-hash, for sub-batch pipelining settings of STORB_RS_EH_SUB
-("<stripes>,<mode>": mode 0 = hash of sub-batch i on a second stream while
-encode i + 1 runs, 1 = interleaved on one stream; unset = encode all, then
-one hash launch). Every setting's digests are checked against the default's,
-and the default's against the host blake3 of a few shares.
+device-resident storb_rs_encode_hashed_dev against encode alone, digests
+checked against the host blake3 of a few shares. (Round 5 also timed
+sub-batch pipelining settings here, a knob since removed:
+profiles/r5d_widehash_pipelining.jsonl.)
 
-usage: python tools/widehash.py [--reps 10] [--subs 8,16,32]
-prints one JSON line per (geometry, setting).
+usage: python tools/widehash.py [--reps 10]
+prints one JSON line per geometry.
 """
 import argparse
 import json
@@ -32,22 +30,17 @@ GEOMS = [  # (k, n, B, stripes): Storb's sizing of 8 MiB / 32 MiB / 4 MiB chunks
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--subs", default="8,16,32")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
     sp = st.cuda_stream
-    settings = [None] + [f"{x},{m}" for x in a.subs.split(",") for m in (0, 1)]
+    settings = [None]
     for k, n, B, ns in GEOMS:
         data = torch.empty(ns * k * B, dtype=torch.uint8, device=dev)
         par = torch.empty(ns * (n - k) * B, dtype=torch.uint8, device=dev)
         hashes = torch.empty(ns * n * 32, dtype=torch.uint8, device=dev)
         ref = None
         for sset in settings:
-            if sset is None:
-                os.environ.pop("STORB_RS_EH_SUB", None)
-            else:
-                os.environ["STORB_RS_EH_SUB"] = sset
             ctx = _lib.Context(0)
             ctx.fill_splitmix_dev(data.data_ptr(), k * B, ns, k * B, 0x5709B, stream=sp)
 
