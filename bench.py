@@ -94,8 +94,9 @@ def parse(argv=None):
                         "'Clock transient'); 0 disables")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--no-traffic", action="store_true",
-                   help="skip the live HBM-traffic passes (rocprofv3 --pmc FETCH_SIZE / "
-                        "WRITE_SIZE on a short child run of the same workload)")
+                   help="skip the live rocprofv3 child passes: HBM traffic (--pmc FETCH_SIZE / "
+                        "WRITE_SIZE) and the kernel trace of the timed region (needed when "
+                        "this run is itself under rocprofv3)")
     p.add_argument("--minimal", action="store_true",
                    help="the timed line only (no traffic passes, copy ceiling, CPU baseline, "
                         "host path, hashing, repair); used for the traffic child runs")
@@ -1688,7 +1689,7 @@ def main():
     ex = line_extras(rank, world, a.minimal, a.config)
     if clocks0 is not None:
         out["roofline"]["gpu_clocks"] = {"before_settle": clocks0, "after_timed_region": clocks1}
-    if "kernel_trace" in ex:
+    if "kernel_trace" in ex and not a.no_traffic:
         kt = kernel_trace(a, w, a.settle_ms)
         if "legs" in kt:
             # without the pre-roll: what a short region right after idle measures

@@ -409,19 +409,24 @@ __device__ __forceinline__ void desc_body(const DescArgs &a, cu64 *rec, uint32_t
   if constexpr (ONE) {
     typedef const PermTab __attribute__((address_space(4))) cPermTab;
     cPermTab *gt = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
-    const DescView v{rec, a.k, a.r};
+    // (Round 5 A/B, not kept: reading the k input pointers in one scalar
+    // load with k a compile-time constant issued the share loads back to back
+    // but measured equal at k = 4 and 32 % slower at k = 16, which then held
+    // 16 pointers in SGPRs; tools/gpu/ab_multi.sh, profiles/r5h_ab_download.txt.)
+    const uint32_t kk = a.k;
+    const DescView v{rec, kk, a.r};
     const uint32_t base = (blockIdx.x % tps) * TILE;
     const uint32_t rr = COPY ? r : static_cast<uint32_t>(RM);
     auto go = [&](auto tabs) __attribute__((always_inline)) {
       if (base + TILE <= cols)
-        perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, a.k, rr, cols,
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, false, COPY>(v, tabs, kk, rr, cols,
                                                           base + threadIdx.x);
       else
-        perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, a.k, rr, cols,
+        perm_tile<KM, RM, T, U, BAR, G, PAIR, true, COPY>(v, tabs, kk, rr, cols,
                                                          base + threadIdx.x);
     };
     if constexpr (TL) {
-      const uint32_t n16 = (COPY && r == 0) ? 0u : a.k * RM * (sizeof(PermTab) / 16);
+      const uint32_t n16 = (COPY && r == 0) ? 0u : kk * RM * (sizeof(PermTab) / 16);
       typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
       for (uint32_t t = threadIdx.x; t < n16; t += T)
         reinterpret_cast<u32x4 *>(lds_ptab)[t] = ((gcu32x4 *)(gt))[t];
@@ -524,19 +529,28 @@ constexpr bool mix_pair() { return KM == 16 || Tune<KM, R>::PAIR; }
 // download's chunks -- most lost 1-3 data shares, each a different set --
 // are one launch: no per-count launch gaps and tails, and no 3-row VALU
 // spent on a 1-row item. Registers: the largest branch's.
+// Workgroup size of the mixed launch. k <= 4 (the default line's download
+// leg): one-wave workgroups, capped at 16 per CU -- the access shape's own
+// ceiling without GF work (tools/dlprobe.hip, profiles/r5e_dlprobe.txt) is
+// 0.799 of 8 TB/s that way against 0.784 for 256-lane workgroups at their
+// best cap (4) and 0.806 for a uniform launch over contiguous stripes.
+template <int KM>
+constexpr int mix_threads() { return KM <= 4 ? 64 : kThreads; }
+
 template <int KM, bool COPY>
-__global__ __launch_bounds__(kThreads) void rs_apply_desc_mix(const DescArgs a) {
+__global__ __launch_bounds__(mix_threads<KM>()) void rs_apply_desc_mix(const DescArgs a) {
   using T1 = Tune<KM, 1>;
+  constexpr int MT = mix_threads<KM>();
   __shared__ __attribute__((aligned(16))) PermTab lds_ptab[T1::TL ? KM * kMixR : 1];
-  const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + kThreads - 1) / kThreads;
+  const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + MT - 1) / MT;
   const uint32_t item = blockIdx.x / tps;  // one tile per workgroup (launch_desc_mix)
   cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
   const uint32_t r = static_cast<uint32_t>(rec[0] >> 32);
 #define STORB_MIX_CASE(R)                                                                   \
   {                                                                                         \
     using C = Tune<KM, R>;                                                                  \
-    static_assert(C::T == kThreads && C::U == 1, "mixed launch: one tile shape");           \
-    desc_body<KM, R, C::T, C::U, C::BAR, mix_g<KM, R>(), C::TL, mix_pair<KM, R>(), COPY, R, \
+    static_assert(C::U == 1, "mixed launch: one column per lane");                          \
+    desc_body<KM, R, MT, C::U, C::BAR, mix_g<KM, R>(), C::TL, mix_pair<KM, R>(), COPY, R,   \
               true>(a, rec, r, lds_ptab);                                                   \
     return;                                                                                 \
   }
@@ -645,11 +659,12 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
 // k <= 4 keeps the RS(4,2) table kernel's measured cap of 4.
 // k = 32 (16 shares per group): 3 per CU, +0.5-0.7 % over uncapped in three
 // interleaved runs (profiles/r4{b,c,d}_mixbench32.txt "G16 cap3").
-constexpr int mix_occ(int KM) { return KM <= 4 ? Tune<4, 2>::OCC : KM == 32 ? 3 : 0; }
+// k <= 4 with one-wave workgroups (mix_threads): 16 per CU.
+constexpr int mix_occ(int KM) { return KM <= 4 ? 16 : KM == 32 ? 3 : 0; }
 
 template <int KM>
 hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
-  constexpr uint64_t TILE = kThreads;
+  constexpr uint64_t TILE = mix_threads<KM>();
   const uint64_t tps = ((a.block >> 4) + TILE - 1) / TILE;
   if (a.tpw != 1) return hipErrorInvalidConfiguration;  // one tile per workgroup
   const uint64_t blocks = ((tps + a.tpw - 1) / a.tpw) * a.nitems;
@@ -657,13 +672,14 @@ hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
   const size_t dyn = cap_lds(a.cap ? static_cast<int>(a.cap) : mix_occ(KM),
                              Tune<KM, 1>::TL ? sizeof(PermTab) * KM * kMixR : 0);
+  const int T = static_cast<int>(TILE);
   if (a.copy) {
     if constexpr (KM <= static_cast<int>(kCopyMaxK))
-      return launch_lds<rs_apply_desc_mix<KM, true>>(blocks, kThreads, dyn, s, a);
+      return launch_lds<rs_apply_desc_mix<KM, true>>(blocks, T, dyn, s, a);
     else
       return hipErrorInvalidValue;
   }
-  return launch_lds<rs_apply_desc_mix<KM, false>>(blocks, kThreads, dyn, s, a);
+  return launch_lds<rs_apply_desc_mix<KM, false>>(blocks, T, dyn, s, a);
 }
 
 template <int KM>

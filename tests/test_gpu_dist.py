@@ -1,0 +1,115 @@
+"""Multi-process HIP path on the GPU box: two rank
+processes, gloo process group, each with its own HIP context on the box's
+GPU (a one-GPU box: both ranks share device 0, as bench.py's STORB_BENCH_DEVICE
+rehearsal does). Each rank encodes its round-robin share of the objects on
+the device (storb_rs_encode_batch_dev) and rebuilds two lost data shares
+(storb_rs_decode_batch_dev); rank 0 gathers every rank's parity digests and
+checks them against the C oracle, and the decode round trips on each rank.
+Then the bench line itself at --gpus 2 (spawned ranks, gloo, shared device).
+"""
+import hashlib
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NOBJ = 12
+K, N, B = 4, 6, 64 << 10
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _obj(i):
+    from oracle import coracle
+    return coracle.splitmix_bytes(0x5709B + i, K * B)
+
+
+def worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from storb_amd import _lib, partition
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = list(partition.objects_for_rank(NOBJ, rank, world))
+        ctx = _lib.Context(0)
+        host = np.concatenate([np.frombuffer(_obj(i), np.uint8) for i in mine])
+        data = torch.from_numpy(host.copy()).to("cuda:0")
+        par = torch.empty(len(mine) * (N - K) * B, dtype=torch.uint8, device="cuda:0")
+        ctx.encode_batch_dev(K, N, B, len(mine), data.data_ptr(), par.data_ptr())
+        ctx.sync()
+        out = torch.zeros_like(data)
+        ctx.decode_batch_dev(K, N, B, len(mine), [2, 3, 4, 5], data.data_ptr(), par.data_ptr(),
+                             out.data_ptr())
+        ctx.sync()
+        roundtrip = bool(torch.equal(out, data))
+        p = par.cpu().numpy().reshape(len(mine), N - K, B)
+        digests = {i: hashlib.sha256(p[j].tobytes()).hexdigest() for j, i in enumerate(mine)}
+        ctx.close()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, {"digests": digests, "roundtrip": roundtrip,
+                                          "pid": os.getpid()})
+        if rank == 0:
+            q.put(gathered)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_processes_encode_on_the_gpu_vs_oracle():
+    import torch.multiprocessing as mp
+
+    from oracle import coracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len({g["pid"] for g in gathered}) == 2
+    assert all(g["roundtrip"] for g in gathered)
+    merged = {}
+    for g in gathered:
+        assert not set(g["digests"]) & set(merged), "object encoded twice"
+        merged.update(g["digests"])
+    assert sorted(merged) == list(range(NOBJ))
+    for i in range(NOBJ):
+        want = coracle.encode(K, N, _obj(i))[0][K:]
+        assert merged[i] == hashlib.sha256(np.ascontiguousarray(want).tobytes()).hexdigest(), i
+
+
+def test_bench_two_ranks_spawned_on_one_gpu():
+    """bench.py --gpus 2 as the driver would start it at N = 2, except that
+    both ranks share the box's one GPU (STORB_BENCH_DEVICE=0, gloo): the line
+    says 2 ranks ran and carries both ranks' GPU time."""
+    env = dict(os.environ, STORB_BENCH_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "5", "--warmup", "1", "--dist-backend", "gloo",
+                        "--chunks", "64", "--cpu-seconds", "0.2", "--settle-ms", "0"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+    assert line["launch"]["pg_ranks"] == 2 and line["launch"]["backend"] == "gloo"
+    assert len(line["per_rank"]) == 2
+    assert all(x["gpu_ms_per_step"] > 0 for x in line["per_rank"])
+    assert line["value"] > 0

@@ -32,6 +32,7 @@ trace config3 --config 3
 trace config4 --config 4
 trace config7 --config 7
 trace config7_erase32 --config 7 --erase 32
+trace config2_download --erase-pattern download
 trace config5_download --config 5 --erase-pattern download
 trace config6_download --config 6 --erase-pattern download
 timeout -k 10 400 python3 bench.py > "$OUT/bench_default.log" 2>&1
