@@ -183,6 +183,7 @@ struct B3Map {
   const uint8_t *in0, *in1;
   uint64_t stride0, stride1, pitch;
   uint32_t per, k;
+  uint32_t out_per, out_off;  // digest of (s, t) at out + (s * out_per + out_off + t) * 32
 };
 
 __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(kB3Threads) void blake3_batch_kernel(
   const uint32_t st = shard / mp.per, t = shard - st * mp.per;
   const uint8_t *p = t < mp.k ? mp.in0 + st * mp.stride0 + static_cast<uint64_t>(t) * mp.pitch
                               : mp.in1 + st * mp.stride1 + static_cast<uint64_t>(t - mp.k) * mp.pitch;
-  uint8_t *o = out + static_cast<uint64_t>(shard) * 32;
+  uint8_t *o = out + (static_cast<uint64_t>(st) * mp.out_per + mp.out_off + t) * 32;
   const uint64_t n = len == 0 ? 1 : (len + b3::kChunkLen - 1) / b3::kChunkLen;
   const bool aligned16 = ((reinterpret_cast<uintptr_t>(p)) & 15) == 0;
   if (n == 1) {  // single chunk: it is the root (one lane per shard, L = 1)
@@ -322,7 +323,7 @@ static hipError_t launch_b3(const B3Map &mp, uint64_t len, uint32_t count, uint8
 
 hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
                                uint64_t stride, uint8_t *out, hipStream_t s) {
-  return launch_b3(B3Map{in, in, stride, stride, 0, 1, 1}, len, count, out, s);
+  return launch_b3(B3Map{in, in, stride, stride, 0, 1, 1, 1, 0}, len, count, out, s);
 }
 
 hipError_t launch_blake3_stripes(const uint8_t *data, uint64_t data_stride, const uint8_t *parity,
@@ -330,8 +331,18 @@ hipError_t launch_blake3_stripes(const uint8_t *data, uint64_t data_stride, cons
                                  uint64_t len, uint32_t nstripes, uint8_t *out, hipStream_t s) {
   if (n == 0 || k > n || static_cast<uint64_t>(nstripes) * n > 0xFFFFFFFFull)
     return hipErrorInvalidValue;
-  return launch_b3(B3Map{data, parity, data_stride, parity_stride, pitch, n, k}, len,
+  return launch_b3(B3Map{data, parity, data_stride, parity_stride, pitch, n, k, n, 0}, len,
                    nstripes * n, out, s);
+}
+
+hipError_t launch_blake3_stripes_part(const uint8_t *base, uint64_t stride, uint64_t pitch,
+                                      uint32_t shares, uint32_t out_per, uint32_t out_off,
+                                      uint64_t len, uint32_t nstripes, uint8_t *out,
+                                      hipStream_t s) {
+  if (shares == 0 || static_cast<uint64_t>(nstripes) * shares > 0xFFFFFFFFull)
+    return hipErrorInvalidValue;
+  return launch_b3(B3Map{base, base, stride, stride, pitch, shares, shares, out_per, out_off},
+                   len, nstripes * shares, out, s);
 }
 
 }  // namespace storb_rs

@@ -105,6 +105,12 @@ hipError_t launch_blake3_batch(const uint8_t *in, uint64_t len, uint32_t count,
 hipError_t launch_blake3_stripes(const uint8_t *data, uint64_t data_stride, const uint8_t *parity,
                                  uint64_t parity_stride, uint64_t pitch, uint32_t k, uint32_t n,
                                  uint64_t len, uint32_t nstripes, uint8_t *out, hipStream_t s);
+// `shares` consecutive shares of each stripe (at base + s * stride + t * pitch),
+// digest of (s, t) at out + (s * out_per + out_off + t) * 32.
+hipError_t launch_blake3_stripes_part(const uint8_t *base, uint64_t stride, uint64_t pitch,
+                                      uint32_t shares, uint32_t out_per, uint32_t out_off,
+                                      uint64_t len, uint32_t nstripes, uint8_t *out,
+                                      hipStream_t s);
 
 // Encode with the blake3 digest of every share in the same pass
 // (rs_encode_hash.hip). Stripe s: data share j at data + s*data_stride +

@@ -1106,7 +1106,11 @@ int storb_rs_encode_hashed_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t
   // (16, 24) x 128 stripes 0.895 ms sequential vs 0.90-1.46 ms
   // (profiles/r5d_widehash_pipelining.jsonl): a sub-batch's hash launch has
   // too few shards to fill the chip, and the encoder's LDS reservation keeps
-  // the two kernels off each other's CUs.
+  // the two kernels off each other's CUs. Hashing the data shares on a second
+  // stream beside the whole encode (parity after it) measured 0.886 ms, and
+  // 0.858 with the encoder uncapped so the two share CUs (1.06x at (16, 24),
+  // none or a loss at (32, 48) / (8, 12); profiles/r5i_widehash.jsonl): not
+  // kept. DESIGN.md §5 has the VALU arithmetic that bounds any overlap.
   const uint32_t p = n - k;
   if (p > 0) {
     std::vector<const uint8_t *> in(k);

@@ -2,8 +2,8 @@
 """Encode + piece ids at Storb's wide geometries: the
 device-resident storb_rs_encode_hashed_dev against encode alone, digests
 checked against the host blake3 of a few shares. (Round 5 also timed
-sub-batch pipelining settings here, a knob since removed:
-profiles/r5d_widehash_pipelining.jsonl.)
+pipelining and concurrency settings here, knobs since removed:
+profiles/r5d_widehash_pipelining.jsonl, profiles/r5i_widehash.jsonl.)
 
 usage: python tools/widehash.py [--reps 10]
 prints one JSON line per geometry.
