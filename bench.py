@@ -858,6 +858,29 @@ def download_leg(ctx, w, stream, a, reps=20):
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "algorithmic_bytes_per_call": alg}}
     if not a.no_traffic:
+        # kernel time of the same mixed launch: a kernel-trace child run with
+        # --erase-pattern download (its decode leg is this call), timed launches only
+        kt = kernel_trace(a, w, a.settle_ms, "download",
+                          [leg_kernel_match(a, w, "encode"), "rs_apply_desc_mix<"])
+        if "legs" in kt:
+            dk = kt["legs"]["decode"]
+            # the child's own survivor sets (Workload, --erase-pattern download, rank 0)
+            from storb_amd import objects
+            rng = np.random.default_rng(SEED_BASE)
+            alg_child = 0
+            for _ in range(N):
+                got = objects.download_arrivals(k, n, rng)
+                e = sum(1 for j in range(k) if j not in sorted(got)[:k])
+                alg_child += (k + e) * B if e else 0
+            res["kernel_trace"] = {"kernel": dk["kernel"], "launches": dk["launches"],
+                                   "avg_us": dk["avg_us"], "median_us": dk["median_us"],
+                                   "algorithmic_bytes_per_launch": alg_child,
+                                   "frac_kernel_time": round(alg_child / (dk["avg_us"] * 1e-6) /
+                                                             1e9 / HBM_PEAK_GBS, 4),
+                                   "call_overhead_us": round(ms * 1e3 - dk["avg_us"], 1),
+                                   "source": kt["source"]}
+        else:
+            res["kernel_trace"] = kt
         t = pmc_download_traffic(a, w)
         res["roofline"]["traffic"] = t.get("traffic")
         res["roofline"]["traffic_source"] = t.get("traffic_source")
@@ -1019,7 +1042,7 @@ def _child(a, erase_pattern, steps=3, warmup=1, settle_ms=0.0):
     return child
 
 
-def kernel_trace(a, w, settle_ms):
+def kernel_trace(a, w, settle_ms, erase_pattern=None, subs=None):
     """One rocprofv3 --kernel-trace --stats child run of exactly this line's
     sequence (same steps, warm-up and settle pre-roll): the launches of the
     timed region, identified from the end of the trace (after it come only
@@ -1041,7 +1064,7 @@ def kernel_trace(a, w, settle_ms):
     try:
         cmd = ["timeout", "-s", "KILL", "150", prof, "--kernel-trace", "--stats",
                "--output-format", "csv", "-d", d, "-o", "run", "--",
-               *_child(a, a.erase_pattern, a.steps, a.warmup, settle_ms)]
+               *_child(a, erase_pattern or a.erase_pattern, a.steps, a.warmup, settle_ms)]
         r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"),
                            stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
         files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
@@ -1053,7 +1076,7 @@ def kernel_trace(a, w, settle_ms):
         shutil.rmtree(d, ignore_errors=True)
     K, probe = a.steps, min(a.steps, 50)
     legs, lo, hi = {}, None, None
-    subs = [leg_kernel_match(a, w, leg) for leg in w.legs]
+    subs = subs or [leg_kernel_match(a, w, leg) for leg in w.legs]
     for li, leg in enumerate(w.legs):
         sub = subs[li]
         # legs that launch the same kernel (config 2: encode and decode are

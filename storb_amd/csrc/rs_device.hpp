@@ -51,6 +51,11 @@ static constexpr int kThreads = 256;
 // (tools/kbench_tune.hip occ). RS(2,1) (Storb's own 256 KiB chunks) and the
 // k = 1 copy measured best uncapped. For 256-lane workgroups caps 2 and 3
 // measure the same, as do 4 and 5: the reservation resolves to even counts.
+// (Round 5: the download-decode probe's finding that one-wave workgroups
+// capped at 16 per CU stream RS(4,2)'s own access shape faster -- 0.852 vs
+// 0.807 of peak with no GF work, tools/dlprobe.hip -- did not carry over to
+// the product kernel: config 2 0.4830 -> 0.4882-0.4913 ms per step at caps 12
+// / 16, config 4 within 0.3 %, profiles/r5m_ab_headline_t64.txt.)
 constexpr int occ_for(int KM, int RM, bool copy) {
   if (copy) {  // fused assembly: config 3's into-a-fresh-buffer decode, pure copy
     if (KM == 8 && RM == 3) return 4;

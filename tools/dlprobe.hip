@@ -271,6 +271,31 @@ int main(int argc, char **argv) {
       // uniform ceiling: contiguous stripes of 4 in + 1 out, same bytes
       CK(hipMalloc(&uni, static_cast<uint64_t>(nitems) * 5 * sh.B));
       CK(hipMemset(uni, 0x11, static_cast<uint64_t>(nitems) * 5 * sh.B));
+      // the headline encode's shape (RS(4,2): 4 in + 2 out, 1024 contiguous
+      // stripes) over workgroup sizes and caps, for the table kernel's shape
+      {
+        uint8_t *u42;
+        const uint64_t ns42 = 1024, bytes42 = ns42 * 6 * sh.B;
+        CK(hipMalloc(&u42, bytes42));
+        CK(hipMemset(u42, 0x22, bytes42));
+        auto add42 = [&](int T, int cap) {
+          const uint32_t blocks = static_cast<uint32_t>(ns42 * (cols / T));
+          vs.push_back(Variant{"encode-shape 4+2 T=" + std::to_string(T) + " cap=" + std::to_string(cap),
+                               static_cast<double>(bytes42),
+                               [=](hipStream_t st) {
+                                 if (T == 256)
+                                   launch<dl_uniform<4, 2, 256>>(blocks, 256, cap_lds(cap), st, u42, cols);
+                                 else if (T == 128)
+                                   launch<dl_uniform<4, 2, 128>>(blocks, 128, cap_lds(cap), st, u42, cols);
+                                 else
+                                   launch<dl_uniform<4, 2, 64>>(blocks, 64, cap_lds(cap), st, u42, cols);
+                               },
+                               {}});
+        };
+        for (int cap : {0, 4, 5}) add42(256, cap);
+        for (int cap : {0, 8, 10}) add42(128, cap);
+        for (int cap : {0, 12, 16, 20}) add42(64, cap);
+      }
       for (int cap : {0, 4})
         vs.push_back(Variant{"uniform contiguous 4+1 T=256 cap=" + std::to_string(cap),
                              static_cast<double>(nitems) * 5 * sh.B,

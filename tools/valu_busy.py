@@ -75,7 +75,7 @@ def main():
         log = d.rstrip("/") + ".log"
         if os.path.exists(log):
             for line in open(log):
-                if line.startswith("{"):
+                if line.startswith("{") and "roofline" in json.loads(line):
                     b = json.loads(line)["roofline"]
                     for leg, kname in b["kernel"].items():
                         for k in s:
