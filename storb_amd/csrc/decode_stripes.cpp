@@ -169,7 +169,13 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
   // the caller's stream is still running (the slot is free: its last use has
   // completed); the decode launches wait for it on the device.
   if (!ctx->desc_stream) {
-    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->desc_stream, hipStreamNonBlocking));
+    // Highest priority: a stream of its own priority class gets a hardware
+    // queue of its own, so the copy can run under the caller's previous
+    // kernel instead of queueing behind it (a default-priority stream can
+    // share the caller's queue: profiles/r5j_download_timeline.txt).
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+    HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->desc_stream, hipStreamNonBlocking, hi));
     HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_copied, hipEventDisableTiming));
   }
   hipError_t e = launch_copy16(dev, hd, total, ctx->desc_stream);

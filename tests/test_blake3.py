@@ -250,3 +250,28 @@ def test_encode_chunks_hashed_zero_copy(ctx, pinned_out):
             assert np.array_equal(par[o:o + B], shares[i]), (c, i)
         for t in range(n):
             assert ids[c, t].tobytes() == _lib.blake3(shares[t].tobytes()), (c, t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n,L,cnt", [
+    (4, 6, 4 * 1001 + 3, 9),       # B = 1002: shares pitched 1008 apart in staging, last padded
+    (16, 24, 16 * 4099 + 5, 5),    # no fused kernel: one hash launch over every share
+    (2, 3, 2 * 333, 4),            # B < one 1 KiB chunk
+])
+def test_encode_chunks_hashed_pitched_staging(ctx, k, n, L, cnt):
+    """storb_rs_encode_chunks_hashed where the share size is not a multiple of
+    16 bytes: the staged shares sit S = round_up(B, 16) apart, so the hash
+    launch covers len = B at pitch S (launch_blake3_stripes), and every
+    digest -- data and parity, in [chunk][share] order -- is the host blake3
+    of the oracle's (zero-padded) share."""
+    from oracle import coracle
+    B = -(-L // k)
+    host = np.concatenate([coracle.splitmix_bytes(0x5709B + 77 * c, L) for c in range(cnt)])
+    par, ids = ctx.encode_chunks_hashed(k, n, host, L, cnt)
+    par = np.asarray(par).reshape(cnt, n - k, B)
+    ids = np.asarray(ids).reshape(cnt, n, 32)
+    for c in range(cnt):
+        shares, _, _ = coracle.encode(k, n, host[c * L:(c + 1) * L])
+        assert np.array_equal(par[c], np.asarray(shares[k:]).reshape(n - k, B)), (k, n, c)
+        for t in range(n):
+            assert ids[c, t].tobytes() == _lib.blake3(np.asarray(shares[t]).tobytes()), (c, t)
