@@ -540,7 +540,11 @@ constexpr bool mix_pair() { return KM == 16 || Tune<KM, R>::PAIR; }
 // 0.799 of 8 TB/s that way against 0.784 for 256-lane workgroups at their
 // best cap (4) and 0.806 for a uniform launch over contiguous stripes.
 template <int KM>
-constexpr int mix_threads() { return KM <= 4 ? 64 : kThreads; }
+#ifndef STORB_MIXT16  // A/B builds
+#define STORB_MIXT16 256
+#define STORB_MIXOCC16 0
+#endif
+constexpr int mix_threads() { return KM <= 4 ? 64 : KM == 16 ? STORB_MIXT16 : kThreads; }
 
 template <int KM, bool COPY>
 __global__ __launch_bounds__(mix_threads<KM>()) void rs_apply_desc_mix(const DescArgs a) {
@@ -665,7 +669,9 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
 // k = 32 (16 shares per group): 3 per CU, +0.5-0.7 % over uncapped in three
 // interleaved runs (profiles/r4{b,c,d}_mixbench32.txt "G16 cap3").
 // k <= 4 with one-wave workgroups (mix_threads): 16 per CU.
-constexpr int mix_occ(int KM) { return KM <= 4 ? 16 : KM == 32 ? 3 : 0; }
+constexpr int mix_occ(int KM) {
+  return KM <= 4 ? 16 : KM == 16 ? STORB_MIXOCC16 : KM == 32 ? 3 : 0;
+}
 
 template <int KM>
 hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
