@@ -540,17 +540,24 @@ constexpr bool mix_pair() { return KM == 16 || Tune<KM, R>::PAIR; }
 // 0.799 of 8 TB/s that way against 0.784 for 256-lane workgroups at their
 // best cap (4) and 0.806 for a uniform launch over contiguous stripes.
 template <int KM>
-#ifndef STORB_MIXT16  // A/B builds
-#define STORB_MIXT16 256
-#define STORB_MIXOCC16 0
-#endif
-constexpr int mix_threads() { return KM <= 4 ? 64 : KM == 16 ? STORB_MIXT16 : kThreads; }
+// k = 16 (config 5's download mix): one-wave workgroups as well, left to
+// their register limit (152 VGPRs: 12 per CU); decode leg 0.1852 -> 0.1829 ms
+// against 256 lanes, where 64 lanes capped at 8 and 128 lanes capped at 4
+// lost 6-8 % (profiles/r5q_ab_k16_mixed_shape.txt, three interleaved rounds).
+// k = 32 keeps 256 lanes capped at 3: one-wave workgroups uncapped or
+// capped at 12 lost 2-3 % on config 6's download leg (0.1736 -> 0.1776-0.1784
+// ms, profiles/r5s_ab_k32_mixed_shape.txt).
+constexpr int mix_threads() { return KM <= 4 || KM == 16 ? 64 : kThreads; }
+// Tables staged in LDS (Tune::TL) in the mixed launch, one-wave workgroups
+// included: read with s_load straight from the constant pool instead, the
+// k = 16 decode leg went 0.1826 -> 0.1878 ms (profiles/r5r_ab_k16_sload_tables.txt).
+template <int KM>
+constexpr bool mix_tl() { return Tune<KM, 1>::TL; }
 
 template <int KM, bool COPY>
 __global__ __launch_bounds__(mix_threads<KM>()) void rs_apply_desc_mix(const DescArgs a) {
-  using T1 = Tune<KM, 1>;
   constexpr int MT = mix_threads<KM>();
-  __shared__ __attribute__((aligned(16))) PermTab lds_ptab[T1::TL ? KM * kMixR : 1];
+  __shared__ __attribute__((aligned(16))) PermTab lds_ptab[mix_tl<KM>() ? KM * kMixR : 1];
   const uint32_t tps = (static_cast<uint32_t>(a.block >> 4) + MT - 1) / MT;
   const uint32_t item = blockIdx.x / tps;  // one tile per workgroup (launch_desc_mix)
   cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
@@ -559,7 +566,7 @@ __global__ __launch_bounds__(mix_threads<KM>()) void rs_apply_desc_mix(const Des
   {                                                                                         \
     using C = Tune<KM, R>;                                                                  \
     static_assert(C::U == 1, "mixed launch: one column per lane");                          \
-    desc_body<KM, R, MT, C::U, C::BAR, mix_g<KM, R>(), C::TL, mix_pair<KM, R>(), COPY, R,   \
+    desc_body<KM, R, MT, C::U, C::BAR, mix_g<KM, R>(), mix_tl<KM>(), mix_pair<KM, R>(), COPY, R, \
               true>(a, rec, r, lds_ptab);                                                   \
     return;                                                                                 \
   }
@@ -669,9 +676,7 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
 // k = 32 (16 shares per group): 3 per CU, +0.5-0.7 % over uncapped in three
 // interleaved runs (profiles/r4{b,c,d}_mixbench32.txt "G16 cap3").
 // k <= 4 with one-wave workgroups (mix_threads): 16 per CU.
-constexpr int mix_occ(int KM) {
-  return KM <= 4 ? 16 : KM == 16 ? STORB_MIXOCC16 : KM == 32 ? 3 : 0;
-}
+constexpr int mix_occ(int KM) { return KM <= 4 ? 16 : KM == 32 ? 3 : 0; }
 
 template <int KM>
 hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
@@ -682,7 +687,7 @@ hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
   const size_t dyn = cap_lds(a.cap ? static_cast<int>(a.cap) : mix_occ(KM),
-                             Tune<KM, 1>::TL ? sizeof(PermTab) * KM * kMixR : 0);
+                             mix_tl<KM>() ? sizeof(PermTab) * KM * kMixR : 0);
   const int T = static_cast<int>(TILE);
   if (a.copy) {
     if constexpr (KM <= static_cast<int>(kCopyMaxK))

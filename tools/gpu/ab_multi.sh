@@ -15,8 +15,8 @@ tail -1 $out/tests.log
 for r in $(seq $rounds); do
   for lib in "${libs[@]}"; do
     tag=$(basename $(dirname $lib))
-    for c in "2 200" "5 100"; do
-      cfg=${c% *}; steps=${c#* }
+    for c in ${CFGS:-"2:200 5:100"}; do
+      cfg=${c%:*}; steps=${c#*:}
       timeout -k 10 120 python tools/lib_ab.py $lib --config $cfg --steps $steps --warmup 10 --erase-pattern download \
         --minimal > $out/c${cfg}_${tag}_$r.json 2>> $out/err.log || exit $?
       python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2], sys.argv[3], d['value'], d['roofline']['leg_ms'])" $out/c${cfg}_${tag}_$r.json c$cfg $tag
