@@ -310,6 +310,32 @@ int main(int argc, char **argv) {
       for (int cap : {0, 8, 12, 16}) add_mix("mix", MIX(16, 64, 1), 64, 1, 1, cap);
       for (uint32_t tpw : {2u, 4u})
         for (int cap : {0, 3}) add_mix("mix", MIX(16, 256, 1), 256, 1, tpw, cap);
+      // the (32, 48) encode's access shape (32 in + 16 out, 1 MiB shares, 32
+      // contiguous stripes: config 6), over workgroup sizes and caps
+      {
+        uint8_t *u3216;
+        const uint64_t B32 = 1u << 20, ns32 = 32, bytes32 = ns32 * 48 * B32;
+        const uint32_t cols32 = static_cast<uint32_t>(B32 / 16);
+        CK(hipMalloc(&u3216, bytes32));
+        CK(hipMemset(u3216, 0x33, bytes32));
+        auto add3216 = [&](int T, int cap) {
+          const uint32_t blocks = static_cast<uint32_t>(ns32 * (cols32 / T));
+          vs.push_back(Variant{"encode-shape 32+16 T=" + std::to_string(T) + " cap=" + std::to_string(cap),
+                               static_cast<double>(bytes32),
+                               [=](hipStream_t st) {
+                                 if (T == 256)
+                                   launch<dl_uniform<32, 16, 256>>(blocks, 256, cap_lds(cap), st, u3216, cols32);
+                                 else if (T == 128)
+                                   launch<dl_uniform<32, 16, 128>>(blocks, 128, cap_lds(cap), st, u3216, cols32);
+                                 else
+                                   launch<dl_uniform<32, 16, 64>>(blocks, 64, cap_lds(cap), st, u3216, cols32);
+                               },
+                               {}});
+        };
+        for (int cap : {0, 2, 3, 4}) add3216(256, cap);
+        for (int cap : {0, 4, 6, 8}) add3216(128, cap);
+        for (int cap : {0, 8, 12, 16}) add3216(64, cap);
+      }
       const uint64_t per = 18ull * sh.B;  // 16 + 2, the mix's mean rows
       CK(hipMalloc(&uni, static_cast<uint64_t>(nitems) * per));
       CK(hipMemset(uni, 0x11, static_cast<uint64_t>(nitems) * per));
