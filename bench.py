@@ -486,7 +486,7 @@ def host_path_rate(ctx, k, n, chunk_bytes, nchunks=256, reps=3, erased=(), sets=
             "decode_pinned_download_value": res.get("decode_pinned_download"),
             "hashed_value": res.get("hashed"), "hashed_pinned_value": res.get("hashed_pinned"),
             "what": f"storb_rs_encode_chunks: {nchunks} x {chunk_bytes >> 20} MiB host chunks "
-                    "-> H2D -> encode -> D2H parity, 2 streams; value = pageable caller "
+                    "-> H2D -> encode -> D2H parity, one stream per copy direction; value = pageable caller "
                     "buffers (staged), pinned_value = page-locked caller buffers (zero-copy kernels); "
                     "hashed_value = storb_rs_encode_chunks_hashed (parity + every share's blake3 "
                     "id computed on the GPU), pageable; hashed_pinned_value = the same from "

@@ -201,6 +201,9 @@ struct storb_rs_ctx {
   storb_rs::detail::PinBuf *pin_out = &pin_out_node[kStagingNodes];
   int pin_node = -1;  // NUMA node of *pin_in / *pin_out (-1: runtime placement)
   storb_rs::detail::PinBuf pipe_in[2], pipe_out[2];
+  // Events of the staged batch pipelines (host_batch.cpp Staging): per
+  // double-buffer slot, H2D done / kernels done / D2H done.
+  hipEvent_t stage_ev[3][2] = {};
   std::map<std::vector<uint8_t>, std::unique_ptr<storb_rs::detail::Tables>> tables;
   size_t table_cap = 1024;  // cached matrices (STORB_RS_TABLE_CACHE), LRU-evicted
   uint64_t table_tick = 0;

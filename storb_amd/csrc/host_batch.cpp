@@ -15,6 +15,57 @@
 using namespace storb_rs;
 using namespace storb_rs::detail;
 
+namespace {
+
+// The staged batch pipelines' device side: H2D on one stream (ctx->pipe[0]),
+// kernels on another (ctx->stream), D2H on a third (ctx->pipe[1]), ordered by
+// events per double-buffer slot. Batch i on stream i % 2 doing H2D -> kernel
+// -> D2H (rounds 1-4) kept the two copy directions from overlapping:
+// tools/sdma_probe.hip measured that arrangement at 50 GB/s of PCIe traffic
+// against 76 GB/s for per-direction streams (profiles/r5w_sdma_probe.txt).
+// Host buffers of slot b (pinned in / out) are reusable once its D2H is
+// done (host_wait); device buffer b once its kernels (for the next H2D)
+// and its D2H (for the next kernel) are done -- both ordered on the device.
+struct Staging {
+  storb_rs_ctx *ctx;
+  hipStream_t in, k, out;
+  bool used[2] = {false, false};
+  explicit Staging(storb_rs_ctx *c) : ctx(c), in(c->pipe[0]), k(c->stream), out(c->pipe[1]) {}
+  hipError_t init() {
+    for (auto &row : ctx->stage_ev)
+      for (auto &e : row)
+        if (!e) {
+          const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+          if (r != hipSuccess) return r;
+        }
+    return hipSuccess;
+  }
+  hipEvent_t ev(int which, int b) const { return ctx->stage_ev[which][b]; }
+  // Host: slot b's pinned buffers are free (its last D2H has landed).
+  hipError_t host_wait(int b) { return used[b] ? hipEventSynchronize(ev(2, b)) : hipSuccess; }
+  // Device: the H2D into slot b may start (the last kernel reading it is done).
+  hipError_t before_in(int b) { return used[b] ? hipStreamWaitEvent(in, ev(1, b), 0) : hipSuccess; }
+  // The kernels of slot b may start after its H2D (and after the last D2H
+  // that read slot b's device outputs).
+  hipError_t after_in(int b) {
+    hipError_t r = hipEventRecord(ev(0, b), in);
+    if (r == hipSuccess) r = hipStreamWaitEvent(k, ev(0, b), 0);
+    if (r == hipSuccess && used[b]) r = hipStreamWaitEvent(k, ev(2, b), 0);
+    return r;
+  }
+  hipError_t after_k(int b) {
+    hipError_t r = hipEventRecord(ev(1, b), k);
+    if (r == hipSuccess) r = hipStreamWaitEvent(out, ev(1, b), 0);
+    return r;
+  }
+  hipError_t after_out(int b) {
+    used[b] = true;
+    return hipEventRecord(ev(2, b), out);
+  }
+};
+
+}  // namespace
+
 extern "C" {
 
 // Pipelined batch encode: two pinned in/out buffer pairs and two streams.
@@ -93,13 +144,15 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                   ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch,
                   static_cast<size_t>(cn) * n * 32);
   };
+  Staging st(ctx);
+  if (!zc) HIP_TRY(ctx, st.init());
   for (uint32_t bi = 0; bi < nb; bi++) {
     const int b = bi & 1;
-    hipStream_t s = ctx->pipe[b];
+    hipStream_t s = zc ? ctx->pipe[b] : st.k;
     // Pinned buffer pair b is free once batch bi-2 has landed (device
-    // buffers are reused in stream order and need no host wait).
+    // buffers are reused in device-side event order and need no host wait).
     if (bi >= 2 && !(in_direct && (out_direct || p == 0) && !hashes_out)) {
-      HIP_TRY(ctx, hipStreamSynchronize(s));
+      HIP_TRY(ctx, zc ? hipStreamSynchronize(s) : st.host_wait(b));
       unpack(bi - 2);
     }
     const uint32_t c0 = bi * batch, cn = std::min(batch, nchunks - c0);
@@ -141,7 +194,9 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     uint8_t *dd = ctx->pipe_dev[b].p;
     uint8_t *dp = dd + per * batch;
     uint8_t *dh = dp + static_cast<size_t>(p) * S * batch;  // digests (if any)
-    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, st.before_in(b));
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, st.in));
+    HIP_TRY(ctx, st.after_in(b));
     hipError_t fe = hipSuccess;
     did_fuse[b] = fused && try_encode_hash(ctx, k, n, B, cn, dd, per, dp,
                                            static_cast<size_t>(p) * S, dh, s, &fe);
@@ -161,16 +216,18 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     if (hashes_out && !did_fuse[b])  // every share of the batch, one launch, [c][t] digests
       HIP_TRY(ctx, launch_blake3_stripes(dd, per, dp, static_cast<size_t>(p) * S, S, k, n, B, cn,
                                          dh, s));
+    HIP_TRY(ctx, st.after_k(b));
     if (back)
       HIP_TRY(ctx, hipMemcpyAsync(out_direct ? parity_out + static_cast<size_t>(c0) * p * B
                                              : ctx->pipe_out[b].p,
-                                  dp, back, hipMemcpyDeviceToHost, s));
+                                  dp, back, hipMemcpyDeviceToHost, st.out));
     if (hashes_out)
       HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p + static_cast<size_t>(p) * S * batch, dh,
-                                  static_cast<size_t>(cn) * n * 32, hipMemcpyDeviceToHost, s));
+                                  static_cast<size_t>(cn) * n * 32, hipMemcpyDeviceToHost, st.out));
+    HIP_TRY(ctx, st.after_out(b));
   }
   for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[bi & 1]));
+    HIP_TRY(ctx, zc ? hipStreamSynchronize(ctx->pipe[bi & 1]) : st.host_wait(bi & 1));
     unpack(bi);
   }
   return STORB_RS_OK;
@@ -240,11 +297,13 @@ static int decode_chunks_grouped(storb_rs_ctx *ctx, uint32_t k, size_t block, si
         put_row(it.chunks[c], it.pat->missing[r], src + (static_cast<size_t>(c) * e + r) * S);
     });
   };
+  Staging st(ctx);
+  HIP_TRY(ctx, st.init());
   for (size_t ii = 0; ii < items.size(); ii++) {
     const int b = ii & 1;
-    hipStream_t s = ctx->pipe[b];
+    hipStream_t s = st.k;
     if (ii >= 2) {  // pinned pair b is free once item ii-2 has landed
-      HIP_TRY(ctx, hipStreamSynchronize(s));
+      HIP_TRY(ctx, st.host_wait(b));
       unpack(ii - 2);
     }
     const Item &it = items[ii];
@@ -262,7 +321,9 @@ static int decode_chunks_grouped(storb_rs_ctx *ctx, uint32_t k, size_t block, si
     });
     uint8_t *dd = ctx->pipe_dev[b].p;
     uint8_t *dm = dd + per * it.cn;
-    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * it.cn, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, st.before_in(b));
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * it.cn, hipMemcpyHostToDevice, st.in));
+    HIP_TRY(ctx, st.after_in(b));
     std::vector<const uint8_t *> in(k);
     std::vector<uint8_t *> o(e);
     std::vector<size_t> ins(k, per), outs(e, static_cast<size_t>(e) * S);
@@ -271,11 +332,13 @@ static int decode_chunks_grouped(storb_rs_ctx *ctx, uint32_t k, size_t block, si
     const int rc = apply(ctx, k, e, it.pat->coef.data(), in.data(), ins.data(), o.data(),
                          outs.data(), S, it.cn, s);
     if (rc) return rc;
+    HIP_TRY(ctx, st.after_k(b));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(e) * S * it.cn,
-                                hipMemcpyDeviceToHost, s));
+                                hipMemcpyDeviceToHost, st.out));
+    HIP_TRY(ctx, st.after_out(b));
   }
   for (size_t ii = items.size() >= 2 ? items.size() - 2 : 0; ii < items.size(); ii++) {
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[ii & 1]));
+    HIP_TRY(ctx, st.host_wait(ii & 1));
     unpack(ii);
   }
   return STORB_RS_OK;
@@ -408,11 +471,13 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   };
   std::vector<const Pattern *> bp;
   std::vector<uint64_t> ptr;
+  Staging st(ctx);
+  HIP_TRY(ctx, st.init());
   for (uint32_t bi = 0; bi < nb; bi++) {
     const int b = bi & 1;
-    hipStream_t s = ctx->pipe[b];
+    hipStream_t s = st.k;
     if (bi >= 2) {  // pinned pair b is free once batch bi-2 has landed
-      HIP_TRY(ctx, hipStreamSynchronize(s));
+      HIP_TRY(ctx, st.host_wait(b));
       unpack(bi - 2);
     }
     const uint32_t c0 = bi * batch, cn = std::min<uint32_t>(batch, static_cast<uint32_t>(staged.size()) - c0);
@@ -428,7 +493,9 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
     });
     uint8_t *dd = ctx->pipe_dev[b].p;
     uint8_t *dm = dd + per * batch;
-    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, s));
+    HIP_TRY(ctx, st.before_in(b));
+    HIP_TRY(ctx, hipMemcpyAsync(dd, hin, per * cn, hipMemcpyHostToDevice, st.in));
+    HIP_TRY(ctx, st.after_in(b));
     bp.assign(cn, nullptr);
     ptr.assign(static_cast<size_t>(cn) * W, 0);
     for (uint32_t c = 0; c < cn; c++) {
@@ -442,11 +509,13 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
     // staged shares are S-pitched: the kernel works on S-byte rows
     const int rc = apply_desc(ctx, k, S, false, bp, ptr, s);
     if (rc) return rc;
+    HIP_TRY(ctx, st.after_k(b));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(emax) * S * cn,
-                                hipMemcpyDeviceToHost, s));
+                                hipMemcpyDeviceToHost, st.out));
+    HIP_TRY(ctx, st.after_out(b));
   }
   for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[bi & 1]));
+    HIP_TRY(ctx, st.host_wait(bi & 1));
     unpack(bi);
   }
   return STORB_RS_OK;

@@ -704,6 +704,9 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     if (p) (void)hipStreamDestroy(p);
   for (auto &e : ctx->slice_ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto &row : ctx->stage_ev)
+    for (auto &e : row)
+      if (e) (void)hipEventDestroy(e);
   if (ctx->desc_stream) {
     (void)hipStreamSynchronize(ctx->desc_stream);
     (void)hipStreamDestroy(ctx->desc_stream);

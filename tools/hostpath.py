@@ -6,6 +6,7 @@ are environment variables the library reads at context creation
 Also the box's PCIe copy rates (bench.py pcie_ceiling) for reference.
 
 usage: STORB_RS_ZC_BATCH=0 python tools/hostpath.py [--k 4 --n 6 --chunk 1048576 --chunks 256]
+       [--lib path/to/libstorb_rs.so]   (another build, for an A/B in one session)
 prints one JSON line.
 """
 import argparse
@@ -28,13 +29,17 @@ def main():
     ap.add_argument("--n", type=int, default=6)
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--chunks", type=int, default=256)
+    ap.add_argument("--lib", default=None)
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
+    if a.lib:
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     ctx = _lib.Context(0)
     erased = [0] if a.n > a.k else []
-    r = bench.host_path_rate(ctx, a.k, a.n, a.chunk, nchunks=a.chunks, erased=erased,
+    r = bench.host_path_rate(ctx, a.k, a.n, a.chunk, nchunks=a.chunks, reps=a.reps, erased=erased,
                              sets=bench.download_sets(a.k, a.n, 64, bench.SEED_BASE + 4343))
     r.pop("what", None)
-    out = {"k": a.k, "n": a.n, "chunk": a.chunk, "chunks": a.chunks,
+    out = {"lib": a.lib, "reps": a.reps, "k": a.k, "n": a.n, "chunk": a.chunk, "chunks": a.chunks,
            "env": {x: os.environ.get(x) for x in ("STORB_RS_ZC_BATCH", "STORB_RS_HOST_THREADS")},
            **r, "pcie": bench.pcie_ceiling(torch.device("cuda", 0))}
     print(json.dumps(out), flush=True)
