@@ -805,7 +805,7 @@ def download_sets(k, n, nchunks, seed, fail=0.0):
     return sets
 
 
-def download_leg(ctx, w, stream, a, reps=20):
+def download_leg(ctx, w, stream, a, reps=100):
     """Storb's real download decode, device-resident, beside the headline
     (outside its timed region): the batch's chunks each keep their own
     survivor set (download_sets), and one storb_rs_decode_stripes_dev call
@@ -834,11 +834,23 @@ def download_leg(ctx, w, stream, a, reps=20):
         raise SystemExit("download decode round trip mismatch")
     del ref
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(3):
+
+    def call():
         ctx.decode_stripes_dev_raw(k, n, B, N, ids, cnt, w.dptr, w.pptr, w.dptr, stream=sp)
+    # the GPU idled through the self-check: the same settle pre-roll as the
+    # headline's timed region (settle_device), or the first ms of calls run
+    # through the power controller's transient
+    settled = settle_device([call], stream, a.settle_ms)
+    stream.synchronize()
+    # the host's own cost of a call (patterns, records, descriptor upload,
+    # launches): 3 calls into an idle descriptor ring, none waits on the GPU
+    h0 = time.perf_counter()
+    for _ in range(3):
+        call()
+    host_us = (time.perf_counter() - h0) * 1e6 / 3
     e0.record(stream)
     for _ in range(reps):
-        ctx.decode_stripes_dev_raw(k, n, B, N, ids, cnt, w.dptr, w.pptr, w.dptr, stream=sp)
+        call()
     e1.record(stream)
     stream.synchronize()
     ms = e0.elapsed_time(e1) / reps
@@ -850,7 +862,8 @@ def download_leg(ctx, w, stream, a, reps=20):
     res = {"value": round(N * w.chunk / GIB / (ms * 1e-3), 2), "unit": "GiB/s",
            "what": "GiB/s of chunks reconstructed (device-resident), per-chunk survivor sets "
                    "from simulated download arrivals, one storb_rs_decode_stripes_dev per batch",
-           "ms_per_call": round(ms, 4), "calls": reps,
+           "ms_per_call": round(ms, 4), "calls": reps, "settle": settled,
+           "host_us_per_call": round(host_us, 1),
            "kernel": f"rs_apply_desc_mix<{min(k, 32)}>",
            "lost_data_shares_histogram": dict(sorted(hist.items())),
            "distinct_patterns": len({tuple(sorted(x)[:k]) for x in sets}),

@@ -338,6 +338,26 @@ HostPool &host_pool(storb_rs_ctx *ctx);
 // of the share in slot s.
 int get_pattern(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint32_t *share_idx,
                 uint32_t nshares, const Pattern **out, std::vector<uint32_t> &slot_pos);
+// get_pattern for the stripes of one call (k, n fixed): stripes whose offered
+// shares are distinct indices < 64 are keyed by the bit set of their first k
+// (what the selection depends on) in a small direct-mapped memo, so a batch
+// of a download's chunks -- a handful of patterns, each offered in many
+// arrival orders -- runs the selection, the key and the cache lookup once per
+// pattern instead of once per stripe. Anything else (duplicates, n > 64, the
+// error cases) goes to get_pattern itself. Valid within one call only.
+class PatternMemo {
+ public:
+  PatternMemo(storb_rs_ctx *ctx, uint32_t k, uint32_t n) : ctx_(ctx), k_(k), n_(n) {}
+  int get(const uint32_t *share_idx, uint32_t nshares, const Pattern **out,
+          std::vector<uint32_t> &slot_pos);
+
+ private:
+  static constexpr uint32_t kSlots = 256;
+  storb_rs_ctx *ctx_;
+  uint32_t k_, n_;
+  uint64_t key_[kSlots] = {};
+  const Pattern *pat_[kSlots] = {};
+};
 // Per-stripe descriptor launches (rs_apply_desc). Item i rebuilds the rows of
 // pattern pats[i] from the k inputs ptr[i*W .. +k) into the outputs
 // ptr[i*W + k .. + e) and, with copy, stores input j also to ptr[i*W + k +

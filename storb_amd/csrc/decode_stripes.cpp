@@ -76,6 +76,40 @@ int get_pattern(storb_rs_ctx *ctx, uint32_t k, uint32_t n, const uint32_t *share
   return STORB_RS_OK;
 }
 
+int PatternMemo::get(const uint32_t *share_idx, uint32_t nshares, const Pattern **out,
+                     std::vector<uint32_t> &slot_pos) {
+  if (n_ > 64 || nshares < k_) return get_pattern(ctx_, k_, n_, share_idx, nshares, out, slot_pos);
+  uint64_t mask = 0;
+  uint8_t pos[64];
+  for (uint32_t i = 0; i < nshares; i++) {
+    const uint32_t id = share_idx[i];
+    if (id >= n_ || (mask >> id & 1)) return get_pattern(ctx_, k_, n_, share_idx, nshares, out, slot_pos);
+    mask |= 1ull << id;
+    pos[id] = static_cast<uint8_t>(i);
+  }
+  // no duplicates: the first k by index are the k lowest set bits
+  uint64_t key = 0, m = mask;
+  for (uint32_t i = 0; i < k_; i++) {
+    const uint64_t low = m & (~m + 1);
+    key |= low;
+    m ^= low;
+  }
+  const uint32_t h = static_cast<uint32_t>((key * 0x9E3779B97F4A7C15ull) >> 56) % kSlots;
+  if (pat_[h] && key_[h] == key) {
+    const Pattern *p = pat_[h];
+    slot_pos.resize(k_);
+    for (uint32_t s = 0; s < k_; s++) slot_pos[s] = pos[p->slot_idx[s]];
+    *out = p;
+    return STORB_RS_OK;
+  }
+  const int rc = get_pattern(ctx_, k_, n_, share_idx, nshares, out, slot_pos);
+  if (rc == STORB_RS_OK) {
+    key_[h] = key;
+    pat_[h] = *out;
+  }
+  return rc;
+}
+
 bool desc_ok(const storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_t block) {
   return ctx->variant != STORB_RS_KERNEL_LDS && k >= 1 && k <= static_cast<uint32_t>(kSlotK) &&
          std::min(k, n - k) <= static_cast<uint32_t>(kSlotR) && block % kAlign == 0;
@@ -128,11 +162,23 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
   size_t total = 0;
   uint64_t tiles = 0;
   const uint64_t tps = (block / 16 + kThreadsTable - 1) / kThreadsTable;
+  // item i's tables within its group's table block (the same pattern in
+  // consecutive items -- the common case -- skips the hash lookup)
+  std::vector<size_t> item_tab(pats.size());
   for (Group *g : groups) {
     g->rec_q = 1 + k + g->r + (copy ? k : 0);
     g->tab_off = total;
-    for (uint32_t i : g->items)
-      if (g->tab_at.emplace(pats[i], g->ntab).second) g->ntab += pats[i]->tabs.size();
+    const Pattern *last = nullptr;
+    size_t last_at = 0;
+    for (uint32_t i : g->items) {
+      if (pats[i] != last) {
+        auto ins = g->tab_at.emplace(pats[i], g->ntab);
+        if (ins.second) g->ntab += pats[i]->tabs.size();
+        last = pats[i];
+        last_at = ins.first->second;
+      }
+      item_tab[i] = last_at;
+    }
     total = round_up(total + g->ntab * sizeof(PermTab), 256);
     g->rec_off = total;
     total = round_up(total + g->items.size() * g->rec_q * 8, 256);
@@ -155,7 +201,7 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
     for (uint32_t i : g->items) {
       const uint64_t *src = &ptr[i * W];
       const uint64_t e = pats[i]->missing.size();
-      rec[0] = static_cast<uint64_t>(g->tab_at[pats[i]]) | (e << 32);
+      rec[0] = static_cast<uint64_t>(item_tab[i]) | (e << 32);
       std::memcpy(rec + 1, src, static_cast<size_t>(k) * 8);
       std::memset(rec + 1 + k, 0, static_cast<size_t>(g->r) * 8);
       std::memcpy(rec + 1 + k, src + k, static_cast<size_t>(e) * 8);
@@ -266,8 +312,9 @@ int storb_rs_decode_stripes_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   std::vector<uint32_t> slot_pos;
   size_t off = 0;
   bool uniform = true;
+  PatternMemo memo(ctx, k, n);
   for (uint32_t st = 0; st < nstripes; st++) {
-    const int rc = get_pattern(ctx, k, n, share_idx + off, nshares[st], &pats[st], slot_pos);
+    const int rc = memo.get(share_idx + off, nshares[st], &pats[st], slot_pos);
     if (rc) {
       ctx->last_error += " (stripe " + std::to_string(st) + ")";
       return rc;

@@ -362,8 +362,9 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   std::vector<const uint8_t *> slot_ptr(static_cast<size_t>(nchunks) * k);
   std::vector<uint32_t> plain, rest, slot_pos;
   size_t off = 0;
+  PatternMemo memo(ctx, k, n);
   for (uint32_t c = 0; c < nchunks; c++) {
-    const int rc = get_pattern(ctx, k, n, share_idx + off, nshares[c], &pats[c], slot_pos);
+    const int rc = memo.get(share_idx + off, nshares[c], &pats[c], slot_pos);
     if (rc) {
       ctx->last_error += " (chunk " + std::to_string(c) + ")";
       return rc;

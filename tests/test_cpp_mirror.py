@@ -55,3 +55,20 @@ def test_sequence_numbers_skip_zero_across_the_wrap():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "seq ok" in r.stdout
+
+
+def test_pattern_memo_matches_get_pattern():
+    """The per-call pattern memo in front of the decode-pattern cache
+    (decode_stripes.cpp PatternMemo) returns what get_pattern returns --
+    pattern, slot positions, error code -- for arrival-ordered share lists
+    with duplicates, too few shares, bad indices and n > 64."""
+    src = os.path.join(ROOT, "tests", "cpp", "test_pattern_memo.cpp")
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "test_pattern_memo")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I" + os.path.join(ROOT, "include"), "-o", exe, src, f"-L{libdir}",
+                    "-lstorb_rs", f"-Wl,-rpath,{libdir}", "-lpthread"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "pattern memo ok" in r.stdout
