@@ -18,6 +18,7 @@
 #include <functional>
 #include <atomic>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -98,6 +99,25 @@ struct PinBuf {
   }
 };
 
+// Order marks of a stream: the events that tell when the launches reading a
+// cached table or a descriptor slot have completed. One event recorded after
+// every launch (rounds 1-4) costs ~1.2 us of queue processing per kernel
+// boundary (profiles/r5g_ab_use_events.txt: headline step +0.5 %, download
+// step +1.0 % without); instead each stream re-records one of kMarks events
+// after every kMarkEvery-th use, and a resource keeps the (stream, use index)
+// of its last use. A mark recorded at or after that index orders after it
+// (stream order); a use no mark covers yet is covered by recording one on
+// that stream when it is the caller's current stream (alive), otherwise by a
+// device synchronisation (storb_rs.cpp covering_mark).
+constexpr int kMarks = 8;
+constexpr uint64_t kMarkEvery = 4;
+struct StreamMarks {
+  hipEvent_t ev[kMarks] = {};
+  uint64_t at[kMarks] = {};  // use index ev[i] was last recorded after (0 = never)
+  unsigned next = 0;
+  uint64_t last = 0;         // newest recorded index
+};
+
 // Device-resident coefficient tables for one (rows x k) matrix, tiled in
 // kSlotR x kSlotK blocks: for block b, ptab + b_off[b] PermTabs and
 // btab + b_off[b]*256 product-table bytes.
@@ -105,9 +125,9 @@ struct PinBuf {
 // Nothing about a table blocks the host: the device copy is allocated
 // stream-ordered (hipMallocAsync) and uploaded on the first caller's stream
 // (`home`); a call on another stream waits for the `uploaded` event on the
-// device. Every stream that launches with the table re-records its own
-// `uses` event, so eviction (LRU, ctx->table_cap entries) can order the
-// hipFreeAsync after the last kernel that reads the table on any stream.
+// device. `uses` holds the table's last use index per stream (StreamMarks),
+// so eviction (LRU, ctx->table_cap entries) can order the hipFreeAsync after
+// the last kernel that reads the table on any stream.
 struct Tables {
   uint8_t *dev = nullptr;
   size_t perm_bytes = 0;
@@ -116,7 +136,7 @@ struct Tables {
   hipStream_t home = nullptr;     // stream the upload was ordered on
   hipEvent_t uploaded = nullptr;  // recorded on `home` after the upload
   bool upload_done = false;
-  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // last use per stream
+  std::vector<std::pair<hipStream_t, uint64_t>> uses;  // last use index per stream
   uint64_t tick = 0;              // LRU clock
   ~Tables() {
     // dev is pool memory (hipMallocAsync). Eviction and context teardown give
@@ -125,7 +145,6 @@ struct Tables {
     // failed itself, after a device synchronisation. Nothing is freed here:
     // a destructor has no stream the free could be ordered on.
     if (uploaded) (void)hipEventDestroy(uploaded);
-    for (auto &u : uses) (void)hipEventDestroy(u.second);
   }
 };
 
@@ -151,7 +170,11 @@ struct Pattern {
   uint64_t tick = 0;
 };
 
-constexpr int kDescRing = 4;   // page-locked descriptor upload buffers per context
+// Descriptor upload slots per context: a slot is reused kDescRing calls
+// later, by when the mark covering its last decode (at most kMarkEvery uses
+// after it) has long completed -- the next copy into the slot waits for that
+// mark on the descriptor stream, not on the caller's queue.
+constexpr int kDescRing = 16;
 // Flags of the events recorded after every launch only to ORDER later work
 // (a table's last use before its free, a descriptor slot's last use before
 // it is rewritten): no system-scope release. A default event's record
@@ -234,12 +257,17 @@ struct storb_rs_ctx {
   uint32_t sbase[storb_rs::kMaxStreamSlices] = {};
   // Decode patterns by (k, n, slot share indices) and the ring the
   // per-stripe descriptors go through: page-locked source, device copy;
-  // desc_ev[i]: the launches of that slot's last use have completed.
+  // desc_use[i]: (stream, use index) of that slot's last decode launches;
+  // desc_cp[i]: recorded on desc_stream after the slot's last copy.
   std::map<std::vector<uint32_t>, std::unique_ptr<storb_rs::detail::Pattern>> patterns;
   uint64_t pattern_tick = 0;
   storb_rs::detail::PinBuf desc_pin[storb_rs::detail::kDescRing];
   storb_rs::detail::DevBuf desc_dev[storb_rs::detail::kDescRing];
-  hipEvent_t desc_ev[storb_rs::detail::kDescRing] = {};
+  std::pair<hipStream_t, uint64_t> desc_use[storb_rs::detail::kDescRing] = {};
+  hipEvent_t desc_cp[storb_rs::detail::kDescRing] = {};
+  // Order marks per stream and the context's use counter (StreamMarks).
+  std::unordered_map<hipStream_t, storb_rs::detail::StreamMarks> marks;
+  uint64_t use_idx = 0;
   hipStream_t desc_stream = nullptr;  // the descriptor copies
   hipEvent_t desc_copied = nullptr;
   unsigned desc_next = 0;
@@ -301,6 +329,15 @@ Variant pick_variant(const storb_rs_ctx *ctx);
 int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
                hipStream_t s, Tables **out);
 int tables_used(storb_rs_ctx *ctx, Tables *t, hipStream_t s);
+// One use of stream s by launches reading a context resource: its index
+// (StreamMarks), recording a mark when due.
+hipError_t stream_used(storb_rs_ctx *ctx, hipStream_t s, uint64_t *use);
+// An event that completes once use `use` on stream s has, or null when none
+// can be had without a device synchronisation: a recorded mark at or after
+// the use, else a mark recorded now when s is `live` (the stream of the
+// current call).
+hipError_t covering_mark(storb_rs_ctx *ctx, hipStream_t s, uint64_t use, hipStream_t live,
+                         hipEvent_t *ev);
 // out_r = sum_j coef[r][j] * in_j for every stripe, tiled onto kernel slots.
 // copy[j] != null (decode into a separate buffer): input j is also stored
 // to copy[j] (by the kernel where it can, else copied first); rows may be 0.

@@ -185,11 +185,20 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
     tiles += tps * g->items.size();
   }
   const uint32_t tpw = desc_tpw(tiles);
-  // Upload slot (page-locked source + device copy), reusable once the
-  // launches of its previous use have completed.
+  // Upload slot (page-locked source + device copy). The page-locked source
+  // is rewritten once the slot's previous copy has completed (host wait, on
+  // the descriptor stream's own event); the device copy is overwritten once
+  // the previous decode launches have (the copy waits for their mark on the
+  // descriptor stream). A slot that must grow is reallocated, and hipFree /
+  // hipHostFree synchronise the device first.
   const unsigned slot = ctx->desc_next++ % kDescRing;
-  if (ctx->desc_ev[slot]) HIP_TRY(ctx, hipEventSynchronize(ctx->desc_ev[slot]));
-  else HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_ev[slot], kOrderEvent));
+  if (ctx->desc_cp[slot]) HIP_TRY(ctx, hipEventSynchronize(ctx->desc_cp[slot]));
+  else HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_cp[slot], kOrderEvent));
+  hipEvent_t prev = nullptr;  // the mark after the slot's previous decode
+  if (ctx->desc_use[slot].second) {
+    HIP_TRY(ctx, covering_mark(ctx, ctx->desc_use[slot].first, ctx->desc_use[slot].second, s, &prev));
+    if (!prev) HIP_TRY(ctx, hipDeviceSynchronize());  // its stream is not this call's: rare
+  }
   HIP_TRY(ctx, ctx->desc_pin[slot].ensure(total));
   HIP_TRY(ctx, ctx->desc_dev[slot].ensure(total));
   uint8_t *h = ctx->desc_pin[slot].p;
@@ -224,7 +233,9 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
     HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->desc_stream, hipStreamNonBlocking, hi));
     HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->desc_copied, hipEventDisableTiming));
   }
-  hipError_t e = launch_copy16(dev, hd, total, ctx->desc_stream);
+  hipError_t e = prev ? hipStreamWaitEvent(ctx->desc_stream, prev, 0) : hipSuccess;
+  if (e == hipSuccess) e = launch_copy16(dev, hd, total, ctx->desc_stream);
+  if (e == hipSuccess) e = hipEventRecord(ctx->desc_cp[slot], ctx->desc_stream);
   if (e == hipSuccess) e = hipEventRecord(ctx->desc_copied, ctx->desc_stream);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, ctx->desc_copied, 0);
   for (size_t gi = 0; e == hipSuccess && gi < groups.size(); gi++) {
@@ -242,8 +253,10 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
     a.mix = g.mix ? 1u : 0u;
     e = launch_apply_desc(a, s);
   }
-  // the slot's reuse event (also after a failed launch: earlier ones may be queued)
-  const hipError_t er = hipEventRecord(ctx->desc_ev[slot], s);
+  // the slot's last use (also after a failed launch: earlier ones may be queued)
+  uint64_t use = 0;
+  const hipError_t er = stream_used(ctx, s, &use);
+  ctx->desc_use[slot] = {s, use};
   if (e != hipSuccess) return hip_fail(ctx, e, "apply_desc");
   if (er != hipSuccess) return hip_fail(ctx, er, "hipEventRecord(descriptors)");
   return STORB_RS_OK;

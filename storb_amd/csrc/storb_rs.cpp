@@ -105,22 +105,32 @@ Variant pick_variant(const storb_rs_ctx *ctx) {
 // pool's own free; a plain hipFree of pool memory (what context teardown did
 // until round 3) is legal only after a device-wide synchronisation and is
 // not used.
-static hipError_t release_table(storb_rs_ctx *ctx, Tables *t) {
+// live: the stream of the current call (a last use on it that no mark
+// covers yet gets one now); null at teardown.
+static hipError_t release_table(storb_rs_ctx *ctx, Tables *t, hipStream_t live) {
   if (!t->dev) return hipSuccess;
   hipError_t e = hipStreamWaitEvent(ctx->stream, t->uploaded, 0);
-  for (auto &u : t->uses)
-    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, u.second, 0);
+  bool sync = false;
+  for (auto &u : t->uses) {
+    hipEvent_t ev = nullptr;
+    if (e == hipSuccess) e = covering_mark(ctx, u.first, u.second, live, &ev);
+    if (e == hipSuccess && ev) e = hipStreamWaitEvent(ctx->stream, ev, 0);
+    sync = sync || !ev;
+  }
+  // a last use on a stream this call does not hold, not yet marked (rare:
+  // the caller moved to other streams right after it)
+  if (e == hipSuccess && sync) e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipFreeAsync(t->dev, ctx->stream);
   if (e == hipSuccess) t->dev = nullptr;
   return e;
 }
 
-static int evict_tables(storb_rs_ctx *ctx) {
+static int evict_tables(storb_rs_ctx *ctx, hipStream_t live) {
   auto victim = ctx->tables.begin();
   for (auto it = ctx->tables.begin(); it != ctx->tables.end(); ++it)
     if (it->second->tick < victim->second->tick) victim = it;
   Tables *t = victim->second.get();
-  HIP_TRY(ctx, release_table(ctx, t));
+  HIP_TRY(ctx, release_table(ctx, t, live));
   // The host source of the upload must outlive the copy; that copy is the
   // oldest work on `home` this table has, long finished in practice.
   HIP_TRY(ctx, hipEventSynchronize(t->uploaded));
@@ -145,16 +155,83 @@ static int tables_ready(storb_rs_ctx *ctx, Tables *t, hipStream_t s) {
   return STORB_RS_OK;
 }
 
+static hipError_t record_mark(StreamMarks &m, hipStream_t s, uint64_t use) {
+  hipEvent_t &e = m.ev[m.next];
+  if (!e) {
+    const hipError_t r = hipEventCreateWithFlags(&e, kOrderEvent);
+    if (r != hipSuccess) return r;
+  }
+  const hipError_t r = hipEventRecord(e, s);
+  if (r != hipSuccess) return r;
+  m.at[m.next] = use;
+  m.last = use;
+  m.next = (m.next + 1) % kMarks;
+  return hipSuccess;
+}
+
+// Marks of streams the context no longer sees (callers' streams come and
+// go): once the map is large, entries whose every mark has completed are
+// dropped; a use on a dropped stream then has no covering mark
+// (covering_mark's null: device synchronisation).
+static void trim_marks(storb_rs_ctx *ctx) {
+  if (ctx->marks.size() < 64) return;
+  for (auto it = ctx->marks.begin(); it != ctx->marks.end();) {
+    bool idle = true;
+    for (hipEvent_t e : it->second.ev) idle = idle && (!e || hipEventQuery(e) == hipSuccess);
+    if (!idle) {
+      ++it;
+      continue;
+    }
+    for (hipEvent_t e : it->second.ev)
+      if (e) (void)hipEventDestroy(e);
+    it = ctx->marks.erase(it);
+  }
+}
+
+hipError_t stream_used(storb_rs_ctx *ctx, hipStream_t s, uint64_t *use) {
+  const uint64_t u = ++ctx->use_idx;
+  *use = u;
+  auto it = ctx->marks.find(s);
+  if (it == ctx->marks.end()) {
+    trim_marks(ctx);
+    it = ctx->marks.emplace(s, StreamMarks{}).first;
+  }
+  StreamMarks &m = it->second;
+  if (m.last && u - m.last < kMarkEvery) return hipSuccess;
+  return record_mark(m, s, u);
+}
+
+hipError_t covering_mark(storb_rs_ctx *ctx, hipStream_t s, uint64_t use, hipStream_t live,
+                         hipEvent_t *ev) {
+  *ev = nullptr;
+  auto it = ctx->marks.find(s);
+  if (it == ctx->marks.end()) return hipSuccess;
+  StreamMarks &m = it->second;
+  if (m.last < use) {  // not marked since that use
+    if (s != live) return hipSuccess;
+    const hipError_t r = record_mark(m, s, ctx->use_idx);
+    if (r != hipSuccess) return r;
+  }
+  // the oldest mark recorded at or after the use (marks are re-recorded in
+  // ring order, so at[] holds the latest index of each)
+  uint64_t best = UINT64_MAX;
+  for (int i = 0; i < kMarks; i++)
+    if (m.ev[i] && m.at[i] >= use && m.at[i] < best) {
+      best = m.at[i];
+      *ev = m.ev[i];
+    }
+  return hipSuccess;
+}
+
 int tables_used(storb_rs_ctx *ctx, Tables *t, hipStream_t s) {
-  for (auto &u : t->uses)
-    if (u.first == s) {
-      HIP_TRY(ctx, hipEventRecord(u.second, s));
+  uint64_t u = 0;
+  HIP_TRY(ctx, stream_used(ctx, s, &u));
+  for (auto &x : t->uses)
+    if (x.first == s) {
+      x.second = u;
       return STORB_RS_OK;
     }
-  hipEvent_t e = nullptr;
-  HIP_TRY(ctx, hipEventCreateWithFlags(&e, kOrderEvent));
-  t->uses.emplace_back(s, e);
-  HIP_TRY(ctx, hipEventRecord(e, s));
+  t->uses.emplace_back(s, u);
   return STORB_RS_OK;
 }
 
@@ -175,7 +252,7 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
     return STORB_RS_OK;
   }
   while (!ctx->tables.empty() && ctx->tables.size() >= std::max<size_t>(ctx->table_cap, 1)) {
-    int rc = evict_tables(ctx);
+    int rc = evict_tables(ctx, s);
     if (rc) return rc;
   }
   auto t = std::make_unique<Tables>();
@@ -680,7 +757,7 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
   DeviceGuard g(ctx->device);
   if (ctx->stream) {
     // tables back to their pool, after every use on any stream
-    for (auto &kv : ctx->tables) (void)release_table(ctx, kv.second.get());
+    for (auto &kv : ctx->tables) (void)release_table(ctx, kv.second.get(), nullptr);
     (void)hipStreamSynchronize(ctx->stream);
   }
   // A table whose stream-ordered release failed: once nothing on the device
@@ -712,11 +789,23 @@ void storb_rs_ctx_destroy(storb_rs_ctx *ctx) {
     (void)hipStreamDestroy(ctx->desc_stream);
     (void)hipEventDestroy(ctx->desc_copied);
   }
-  for (auto &e : ctx->desc_ev)  // descriptor launches may run on callers' streams
-    if (e) {
-      (void)hipEventSynchronize(e);
-      (void)hipEventDestroy(e);
-    }
+  // a descriptor slot's last decode no mark covers (on a caller's stream)
+  bool desc_sync = false;
+  for (auto &u : ctx->desc_use) {
+    hipEvent_t ev = nullptr;
+    if (u.second && covering_mark(ctx, u.first, u.second, nullptr, &ev) == hipSuccess && !ev)
+      desc_sync = true;
+  }
+  if (desc_sync) (void)hipDeviceSynchronize();
+  for (auto &e : ctx->desc_cp)
+    if (e) (void)hipEventDestroy(e);
+  // descriptor launches may run on callers' streams: their last marks
+  for (auto &kv : ctx->marks)
+    for (hipEvent_t e : kv.second.ev)
+      if (e) {
+        (void)hipEventSynchronize(e);
+        (void)hipEventDestroy(e);
+      }
   // Unfinished async ops: their device work ends here (the slot streams are
   // drained below) and they are cut loose from the context, so a later
   // storb_rs_op_test / _finish returns STORB_RS_ECLOSED without touching it.

@@ -268,3 +268,44 @@ def test_decode_chunks_tiny_shares_many_lost(ctx, L):
     got = ctx.decode_chunks(k, n, B, pad, batch)
     for c in range(3):
         assert np.array_equal(got[c], objs[c]), (L, c)
+
+
+@pytest.mark.gpu
+def test_descriptor_slots_reused_across_streams(ctx):
+    """The descriptor upload ring (decode_stripes.cpp; ctx.hpp kDescRing) on
+    sparse order marks (StreamMarks): calls hop between streams -- one of them
+    a raw HIP stream destroyed after its last call, one used a single time,
+    the null stream -- with ~1 ms of encodes queued ahead now and then, so a
+    slot's previous decode may still be queued when the slot comes round
+    again. Every call writes its own output buffer, each checked against the
+    original data."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    k, n, B, ns = 4, 6, 64 << 10, 96
+    data, par = oracle_stripes(k, n, B, ns, 4242)
+    sets = download_sets(k, n, ns, 4343)
+    dd = torch.from_numpy(data.reshape(-1).copy()).to(DEV)
+    dp = torch.from_numpy(par.reshape(-1).copy()).to(DEV)
+    big = torch.zeros(512 << 20, dtype=torch.uint8, device=DEV)
+    bigp = torch.zeros(256 << 20, dtype=torch.uint8, device=DEV)
+    a, b, once = (torch.cuda.Stream(device=DEV) for _ in range(3))
+    raw = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(raw), 1) == 0
+    plan = ["raw"] * 3 + ["a"] * 5 + ["once"] + ["b"] * 20 + ["a", "b"] * 10 + ["null"] * 3 + \
+        ["a"] * 17
+    outs = [torch.full_like(dd, 0x3C) for _ in plan]
+    torch.cuda.synchronize()
+    for i, name in enumerate(plan):
+        sp = {"a": a.cuda_stream, "b": b.cuda_stream, "once": once.cuda_stream, "null": None,
+              "raw": raw.value}[name]
+        if i % 7 == 0:  # queue work ahead of the decode on this stream
+            ctx.encode_batch_dev(4, 6, 1 << 20, 128, big.data_ptr(), bigp.data_ptr(), stream=sp)
+        ctx.decode_stripes_dev(k, n, B, sets, dd.data_ptr(), dp.data_ptr(), outs[i].data_ptr(),
+                               stream=sp)
+        if name == "raw" and plan[i + 1] != "raw":
+            assert hip.hipStreamSynchronize(raw) == 0
+            assert hip.hipStreamDestroy(raw) == 0
+    torch.cuda.synchronize()
+    ref = torch.from_numpy(data.reshape(-1).copy()).to(DEV)
+    for i, out in enumerate(outs):
+        assert torch.equal(out, ref), (i, plan[i])
