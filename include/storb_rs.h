@@ -198,7 +198,11 @@ int storb_rs_host_is_pinned(const void *p, size_t len);
  * share p at d_parity + s*parity_stride + p*block. Strides of 0 mean the
  * packed defaults k*block and (n-k)*block. Asynchronous on `hip_stream`
  * (a hipStream_t; NULL = the HIP null stream, which orders with the
- * device's legacy default stream). */
+ * device's legacy default stream). The context records an order event on
+ * `hip_stream` only now and then (every few calls), never on a stream it is
+ * not being called with: a caller may destroy its stream once the work on it
+ * has completed, and a context resource last used there is then reclaimed
+ * after a device synchronisation. */
 int storb_rs_encode_batch_dev(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
                               size_t block, uint32_t nstripes,
                               const uint8_t *d_data, size_t data_stride,
