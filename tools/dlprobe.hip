@@ -8,14 +8,16 @@
 //        that lost one data share (bench.py --erase-pattern download, seed
 //        0x5709B) -- a 4 read : 1 write mix over a scattered subset;
 //   k16: config 5's shape, 128 x 8 MiB chunks (B = 512 KiB), 48 / 58 / 9
-//        chunks that lost 1 / 2 / 3 data shares -- 16 : 1-3.
+//        chunks that lost 1 / 2 / 3 data shares -- 16 : 1-3;
+//   k32: config 6's shape, 32 x 32 MiB chunks (B = 1 MiB), 14 / 13 / 1 chunks
+//        that lost 1 / 2 / 3 data shares -- 32 : 1-3.
 // Variants (all moving the same bytes): workgroup size T, 16-B columns per
 // lane U, tiles per workgroup, resident-workgroup cap (LDS reservation),
 // record read through scalar loads vs computed addresses (a uniform launch
 // over contiguous stripes, the ceiling with no records at all). Each sample
 // times `reps` back-to-back launches; interleaved rounds, median.
 //
-// build: make -C tools dlprobe   run: tools/_build/dlprobe [rounds] [reps]
+// build: make -C tools dlprobe   run: tools/_build/dlprobe [rounds] [reps] [k4|k16|k32]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,7 +42,7 @@
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const uint64_t __attribute__((address_space(4))) cu64;
 
-constexpr int kMaxK = 16, kMaxR = 4;
+constexpr int kMaxK = 32, kMaxR = 4;
 // One item: r (low 32 bits of q[0] >> 32), k input pointers, kMaxR outputs.
 constexpr int kRecQ = 1 + kMaxK + kMaxR;
 
@@ -181,13 +183,16 @@ int main(int argc, char **argv) {
   const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
   const int reps = argc > 2 ? std::atoi(argv[2]) : 8;
   std::vector<Shape> shapes = {{"k4", 4, 6, 1024, 256u << 10, {349, 675}},
-                               {"k16", 16, 24, 128, 512u << 10, {13, 48, 58, 9}}};
+                               {"k16", 16, 24, 128, 512u << 10, {13, 48, 58, 9}},
+                               {"k32", 32, 48, 32, 1u << 20, {4, 14, 13, 1}}};
+  const char *only = argc > 3 ? argv[3] : nullptr;  // run one shape
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (const Shape &sh : shapes) {
+    if (only && std::string(only) != sh.name) continue;
     const uint64_t chunk = sh.k * sh.B;
     uint8_t *data, *par, *uni;
     CK(hipMalloc(&data, sh.nchunks * chunk));
@@ -251,8 +256,10 @@ int main(int argc, char **argv) {
                            [=](hipStream_t st) {
                              if (K == 4)
                                launch<dl_persist<4, 256, 1>>(grid, T, dyn, st, a, total);
-                             else
+                             else if (K == 16)
                                launch<dl_persist<16, 256, 1>>(grid, T, dyn, st, a, total);
+                             else
+                               launch<dl_persist<32, 256, 1>>(grid, T, dyn, st, a, total);
                            },
                            {}});
     };
@@ -302,6 +309,21 @@ int main(int argc, char **argv) {
                              [=](hipStream_t st) {
                                launch<dl_uniform<4, 1, 256>>(nitems * (cols / 256), 256,
                                                              cap_lds(cap), st, uni, cols);
+                             },
+                             {}});
+    } else if (sh.k == 32) {
+      for (int cap : {0, 2, 3, 4}) add_mix("mix", MIX(32, 256, 1), 256, 1, 1, cap);
+      for (int cap : {0, 4, 6, 8}) add_mix("mix", MIX(32, 128, 1), 128, 1, 1, cap);
+      for (int cap : {0, 8, 12, 16}) add_mix("mix", MIX(32, 64, 1), 64, 1, 1, cap);
+      const uint64_t per = 34ull * sh.B;  // 32 + 2, the mix's mean rows
+      CK(hipMalloc(&uni, static_cast<uint64_t>(nitems) * per));
+      CK(hipMemset(uni, 0x11, static_cast<uint64_t>(nitems) * per));
+      for (int cap : {0, 3})
+        vs.push_back(Variant{"uniform contiguous 32+2 T=256 cap=" + std::to_string(cap),
+                             static_cast<double>(nitems) * per,
+                             [=](hipStream_t st) {
+                               launch<dl_uniform<32, 2, 256>>(nitems * (cols / 256), 256,
+                                                              cap_lds(cap), st, uni, cols);
                              },
                              {}});
     } else {
