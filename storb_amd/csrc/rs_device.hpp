@@ -253,6 +253,10 @@ template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD,
           bool COPY = false, class V, class TP>
 __device__ __forceinline__ void perm_tile(const V &v, TP tabs, uint32_t k,
                                           uint32_t r, uint32_t cols, uint32_t c0) {
+  // the groups cover the bucket's KM input slots (inputs >= k skipped): a G
+  // that does not divide KM would drop the last KM % G inputs (a G = 12 A/B
+  // build at k = 32 failed the bench's round-trip check, round 5)
+  static_assert(KM % G == 0, "load group size must divide the k bucket");
   constexpr int NG = KM / G;
   u32x4 buf[2][G][U];
   u32x4 acc[RM][U];
