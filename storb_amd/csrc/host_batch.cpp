@@ -130,7 +130,7 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     if (p > 0 && !out_direct) {
       if (S == B) {
         pool.copy(parity_out + static_cast<size_t>(c0) * p * B, ctx->pipe_out[b].p,
-                  static_cast<size_t>(cn) * p * B);
+                  static_cast<size_t>(cn) * p * B, true);
       } else {
         pool.run(static_cast<int>(cn), [&](int c) {
           for (uint32_t i = 0; i < p; i++)
@@ -161,7 +161,7 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
     if (in_direct) {
       // the H2D below reads the caller's page-locked chunks in place
     } else if (packed) {
-      pool.copy(ctx->pipe_in[b].p, data + static_cast<size_t>(c0) * chunk_len, per * cn);
+      pool.copy(ctx->pipe_in[b].p, data + static_cast<size_t>(c0) * chunk_len, per * cn, true);
     } else {
       pool.run(static_cast<int>(cn), [&](int c) {
         const uint8_t *src = data + (static_cast<size_t>(c0) + c) * chunk_len;
@@ -261,7 +261,7 @@ static int decode_chunks_grouped(storb_rs_ctx *ctx, uint32_t k, size_t block, si
   auto put_row = [&](uint32_t c, uint32_t row, const uint8_t *src) {
     const size_t o = static_cast<size_t>(row) * block;
     if (o < outlen)
-      std::memcpy(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
+      copy_nt(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
   };
   std::map<const Pattern *, std::vector<uint32_t>> groups;
   for (uint32_t c : rest) groups[pats[c]].push_back(c);
@@ -314,7 +314,7 @@ static int decode_chunks_grouped(storb_rs_ctx *ctx, uint32_t k, size_t block, si
       for (uint32_t sl = 0; sl < k; sl++) {
         const uint8_t *src = slot_ptr[static_cast<size_t>(ch) * k + sl];
         uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(sl) * S;
-        std::memcpy(dst, src, block);
+        copy_nt(dst, src, block);
         if (S > block) std::memset(dst + block, 0, S - block);
         if (it.pat->slot_idx[sl] == sl) put_row(ch, sl, src);  // present data share
       }
@@ -382,7 +382,7 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
   auto put_row = [&](uint32_t c, uint32_t row, const uint8_t *src) {
     const size_t o = static_cast<size_t>(row) * block;
     if (o < outlen)
-      std::memcpy(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
+      copy_nt(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
   };
   if (!plain.empty())  // all data shares present: concatenation (zfec does the same)
     pool.run(static_cast<int>(plain.size()), [&](int i) {
@@ -487,7 +487,7 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
       const uint32_t ch = staged[c0 + c];
       for (uint32_t sl = 0; sl < k; sl++) {
         uint8_t *dst = hin + static_cast<size_t>(c) * per + static_cast<size_t>(sl) * S;
-        std::memcpy(dst, sp(ch, sl), block);
+        copy_nt(dst, sp(ch, sl), block);
         if (S > block) std::memset(dst + block, 0, S - block);
         if (pats[ch]->slot_idx[sl] == sl) put_row(ch, sl, sp(ch, sl));  // present data share
       }

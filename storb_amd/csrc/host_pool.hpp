@@ -17,6 +17,9 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 namespace storb_rs {
 
@@ -29,6 +32,49 @@ struct CopySeg {
   const uint8_t *src;
   size_t len;
 };
+
+// memcpy with non-temporal 32-byte stores (AVX2; plain memcpy without it or
+// below 256 KiB): no read-for-ownership of the destination lines. The batch
+// pipelines (host_batch.cpp) copy this way into staging and into the
+// caller's output: pageable batch decode 18-25 -> 32-35 GiB/s, encode equal
+// (tools/gpu/hostpath_ab.sh, profiles/r5nt_hostpath_nt_ab.jsonl, staging
+// only, and r5nt_hostpath_nt_output_ab.jsonl, output rows too). The
+// single-chunk calls keep memcpy (their 8 MiB encode lost with NT stores,
+// below).
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) inline void nt_copy_avx2(uint8_t *d, const uint8_t *s, size_t n) {
+  size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
+  if (head > n) head = n;
+  std::memcpy(d, s, head);
+  d += head;
+  s += head;
+  n -= head;
+  const size_t m = n & ~static_cast<size_t>(127);
+  for (size_t i = 0; i < m; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 64));
+    const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(s + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i *>(d + i + 96), e);
+  }
+  std::memcpy(d + m, s + m, n - m);
+  _mm_sfence();
+}
+#endif
+inline void copy_nt(void *dst, const void *src, size_t n) {
+#if defined(__x86_64__)
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2 && n >= (256u << 10)) {
+    nt_copy_avx2(static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), n);
+    return;
+  }
+#endif
+  std::memcpy(dst, src, n);
+}
+
 
 class HostPool {
  public:
@@ -78,9 +124,9 @@ class HostPool {
   }
 
   // memcpy split over the pool (copy_segs' rule).
-  void copy(void *dst, const void *src, size_t bytes) {
+  void copy(void *dst, const void *src, size_t bytes, bool nt = false) {
     CopySeg s{static_cast<uint8_t *>(dst), static_cast<const uint8_t *>(src), bytes};
-    copy_segs(&s, 1);
+    copy_segs(&s, 1, nt);
   }
 
   // How many threads a copy of `total` bytes into page-locked memory takes.
@@ -104,7 +150,7 @@ class HostPool {
 
   // Copy / zero-fill a list of byte ranges, the total split evenly over
   // parts_for(total) threads.
-  void copy_segs(const CopySeg *segs, size_t nsegs) {
+  void copy_segs(const CopySeg *segs, size_t nsegs, bool nt = false) {
     size_t total = 0;
     for (size_t i = 0; i < nsegs; i++) total += segs[i].len;
     if (total == 0) return;
@@ -117,7 +163,8 @@ class HostPool {
         const CopySeg &sg = segs[i];
         if (base + sg.len > lo) {
           const size_t a = lo - base, b = std::min(sg.len, hi - base);
-          if (sg.src) std::memcpy(sg.dst + a, sg.src + a, b - a);
+          if (sg.src && nt) copy_nt(sg.dst + a, sg.src + a, b - a);
+          else if (sg.src) std::memcpy(sg.dst + a, sg.src + a, b - a);
           else std::memset(sg.dst + a, 0, b - a);
           lo = base + b;
         }
