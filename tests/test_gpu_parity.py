@@ -738,3 +738,47 @@ def test_concurrent_calls_per_thread_and_shared_context():
         x.join()
     shared.close()
     assert not errors, errors[:3]
+
+
+@pytest.mark.parametrize("zc", ["1", "0"])
+def test_host_batches_reuse_staging_slots(zc, monkeypatch):
+    """Several 64 MiB batches per call, so each double-buffer slot of the
+    staged pipelines (host_batch.cpp Staging: H2D, kernels and D2H on a
+    stream each, event-ordered per slot; non-temporal host copies) is reused:
+    pageable encode (with and without piece ids) against the oracle's parity,
+    pageable and page-locked download-pattern decode against the data."""
+    monkeypatch.setenv("STORB_RS_ZC_BATCH", zc)
+    ctx = _lib.Context(0)
+    try:
+        k, n, L, cnt = 4, 6, 1 << 20, 200  # 200 MiB: four batches
+        B = L // k
+        data = rnd(L * cnt, 4242 + int(zc))
+        want = coracle.encode_parity_many(k, n, data, L, cnt, threads=8).reshape(cnt, n - k, B)
+        par = ctx.encode_chunks(k, n, data, L, cnt).reshape(cnt, n - k, B)
+        assert np.array_equal(par, want)
+        ids = np.zeros((cnt, n, 32), np.uint8)
+        par2 = np.zeros_like(par.reshape(-1))
+        ctx.encode_chunks_hashed(k, n, data, L, cnt, out=par2, hashes=ids)
+        assert np.array_equal(par2.reshape(cnt, n - k, B), want)
+        for c in (0, 63, 64, 127, 128, cnt - 1):  # a chunk in every batch
+            assert bytes(ids[c, 0]) == _lib.blake3(data[c * L:c * L + B].tobytes())
+            assert bytes(ids[c, k]) == _lib.blake3(want[c, 0].tobytes())
+        rng = random.Random(7)
+        dat = data.reshape(cnt, k, B)
+        chunks = []
+        for c in range(cnt):
+            sel = rng.sample(range(n), k + 1)
+            chunks.append(([dat[c, i] if i < k else want[c, i - k] for i in sel], sel))
+        got = ctx.decode_chunks(k, n, B, 0, chunks)
+        assert np.array_equal(got.reshape(-1), data)
+        pin = _lib.PinnedBuffer(L * cnt)
+        try:
+            rec = pin.array.reshape(cnt, L)
+            rec[:] = 0
+            ctx.decode_chunks(k, n, B, 0, chunks, out=rec)
+            assert np.array_equal(rec.reshape(-1), data)
+        finally:
+            rec = None
+            pin.free()
+    finally:
+        ctx.close()
