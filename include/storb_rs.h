@@ -92,6 +92,9 @@ typedef struct {
   uint64_t sliced_calls;     /* single calls on the column-sliced path */
   uint64_t live_ops;         /* async ops started and not finished */
   uint64_t tables;           /* cached coefficient tables */
+  uint64_t device_syncs;     /* device-wide syncs the stream-ordering fallbacks took (rare) */
+  int32_t caller_node;       /* NUMA node of the thread that created the context, -1 unknown */
+  int32_t device_node;       /* NUMA node of the context's GPU, -1 unknown */
 } storb_rs_ctx_stats_t;
 int storb_rs_ctx_stats(const storb_rs_ctx *ctx, storb_rs_ctx_stats_t *out);
 /* Bytes in use / reserved in the device's default stream-ordered memory pool

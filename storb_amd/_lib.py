@@ -60,7 +60,9 @@ class JitStats(C.Structure):
 class CtxStats(C.Structure):
     """storb_rs_ctx_stats_t (include/storb_rs.h)."""
     _fields_ = [("streamed_calls", C.c_uint64), ("stream_fallbacks", C.c_uint64),
-                ("sliced_calls", C.c_uint64), ("live_ops", C.c_uint64), ("tables", C.c_uint64)]
+                ("sliced_calls", C.c_uint64), ("live_ops", C.c_uint64), ("tables", C.c_uint64),
+                ("device_syncs", C.c_uint64), ("caller_node", C.c_int32),
+                ("device_node", C.c_int32)]
 
 
 NOTIFY_FN = C.CFUNCTYPE(None, vp)  # storb_rs_notify_fn

@@ -280,6 +280,16 @@ struct storb_rs_ctx {
   std::set<storb_rs_op *> live_ops;
   // Single-call path counters (storb_rs_ctx_stats).
   std::atomic<uint64_t> n_streamed{0}, n_stream_fallbacks{0}, n_sliced{0};
+  // Device-wide synchronisations the ordering fallbacks took (a table's or a
+  // descriptor slot's last use on a stream no mark covers): rare by design,
+  // counted so a caller-stream pattern that hits them shows.
+  std::atomic<uint64_t> n_device_syncs{0};
+  // tables.size(), kept beside the map (updated under mu) so storb_rs_ctx_stats
+  // reads it without waiting for a call that holds mu.
+  std::atomic<uint64_t> n_tables{0};
+  // NUMA node of the thread that created the context (-1 unknown) and of the
+  // device it got: storb_rs_ctx_create(-1) picks among the caller's node's GPUs.
+  int create_node = -1, device_node = -1;
   // Streamed single calls: how long a workgroup waits for its slice's ready
   // word (s_memrealtime ticks, 100 MHz) and how long the host waits for a
   // done word before it drains the stream and looks again (ms). Test knob

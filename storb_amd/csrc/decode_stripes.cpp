@@ -197,7 +197,10 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
   hipEvent_t prev = nullptr;  // the mark after the slot's previous decode
   if (ctx->desc_use[slot].second) {
     HIP_TRY(ctx, covering_mark(ctx, ctx->desc_use[slot].first, ctx->desc_use[slot].second, s, &prev));
-    if (!prev) HIP_TRY(ctx, hipDeviceSynchronize());  // its stream is not this call's: rare
+    if (!prev) {  // its stream is not this call's: rare (counted, storb_rs_ctx_stats)
+      ctx->n_device_syncs++;
+      HIP_TRY(ctx, hipDeviceSynchronize());
+    }
   }
   HIP_TRY(ctx, ctx->desc_pin[slot].ensure(total));
   HIP_TRY(ctx, ctx->desc_dev[slot].ensure(total));

@@ -312,12 +312,26 @@ static void use_caller_staging(storb_rs_ctx *ctx) {
   if (node == -2) node = cpu_numa_node(sched_getcpu());
   const int slot = node >= 0 && node < storb_rs_ctx::kStagingNodes ? node
                                                                   : storb_rs_ctx::kStagingNodes;
-  if (ctx->pin_in != &ctx->pin_in_node[slot])
+  if (ctx->pin_in != &ctx->pin_in_node[slot]) {
+    bool drained = false;
     for (int i = 0; i <= storb_rs_ctx::kStagingNodes; i++) {
       if (i == slot) continue;
+      if (ctx->pin_in_node[i].cap <= kStagingKeep && ctx->pin_out_node[i].cap <= kStagingKeep)
+        continue;
+      // Every path that stages syncs or drains before it returns today; the
+      // release still waits for the context's own streams (once, only on a
+      // node switch), so a later asynchronous path cannot leave a copy or a
+      // zero-copy kernel on unmapped memory.
+      if (!drained) {
+        (void)hipStreamSynchronize(ctx->stream);
+        for (hipStream_t s : ctx->pipe)
+          if (s) (void)hipStreamSynchronize(s);
+        drained = true;
+      }
       if (ctx->pin_in_node[i].cap > kStagingKeep) ctx->pin_in_node[i].release();
       if (ctx->pin_out_node[i].cap > kStagingKeep) ctx->pin_out_node[i].release();
     }
+  }
   ctx->pin_in = &ctx->pin_in_node[slot];
   ctx->pin_out = &ctx->pin_out_node[slot];
   ctx->pin_node = slot < storb_rs_ctx::kStagingNodes ? node : -1;

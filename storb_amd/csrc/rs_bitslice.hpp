@@ -112,6 +112,28 @@ struct BsTune {
   static constexpr size_t LDS = SPLIT ? split_lds_bytes(kSplitGroup) : 0;
 };
 
+// Input-split workgroups (rs_bitslice_core.h bs_ksplit_body) for the batch
+// encoders: C column groups of W waves, G shares per load group, CAP resident
+// per CU (LDS and registers cap it lower: (16, 24) holds 3 of its 256-lane
+// workgroups per CU). tools/bstune.hip BSTUNE_KSPLIT, three sweeps
+// (profiles/r6c_bstune_ksplit.txt, r6e_*): (16, 24) 79.3-80.1 % -> 81.0-81.7 %
+// of 8 TB/s (C = 1, W = 4), (32, 48) 74.0 -> 75.4 % (C = 2, W = 2); the same
+// shapes with no GF work stream at 81.8 / 75.5 % (r6d_bstune_nogf.txt), the
+// one-wave tiles at 80.1 / 77.4 %.
+template <int K, int N>
+struct KsTune {
+  static constexpr bool ON = (K == 16 && N == 24) || (K == 32 && N == 48);
+  static constexpr int C = K == 16 ? 1 : 2, W = K == 16 ? 4 : 2, G = 4, CAP = K == 16 ? 4 : 2;
+  static constexpr uint64_t CPT = 128u * C;
+};
+
+template <int K, int N>
+__global__ __launch_bounds__((64 * KsTune<K, N>::C * KsTune<K, N>::W)) void rs_encode_bitslice_ks(
+    const ApplyArgs a) {
+  using S = KsTune<K, N>;
+  bs_ksplit_body<EncMat<K, N>, S::C, S::W, S::G, 1>(a);
+}
+
 template <int K, int N>
 __global__ __launch_bounds__((BsTune<K, N>::T)) __attribute__((amdgpu_waves_per_eu(2))) void
 rs_encode_bitslice(const ApplyArgs a) {
@@ -164,6 +186,15 @@ hipError_t launch_bitslice_split(const ApplyArgs &a, hipStream_t s) {
 
 template <int K, int N>
 hipError_t launch_bitslice(const ApplyArgs &a, hipStream_t s) {
+  if constexpr (KsTune<K, N>::ON) {
+    using S = KsTune<K, N>;
+    const uint64_t blocks = (((a.block >> 4) + S::CPT - 1) / S::CPT) * a.nstripes;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+    return launch_lds<rs_encode_bitslice_ks<K, N>>(
+        blocks, 64 * S::C * S::W, cap_lds(wg_cap(S::CAP), ksplit_lds_bytes(S::C, S::W, N - K)), s,
+        a);
+  }
   using C = BsTune<K, N>;
   constexpr uint64_t cpt = C::CPT;
   const uint64_t cols = a.block >> 4;

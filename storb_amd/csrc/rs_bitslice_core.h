@@ -390,6 +390,129 @@ __device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
     bs_split_wave<M, G, 1>(a, stripe, v0, cols, lane, lds.v);
 }
 
+// ------------------------------------------------------------ input-split form
+// A workgroup of C x W waves covers C x 2 KiB (128 16-B columns per column
+// group) of every share. The W waves of a column group cover the SAME 2 KiB
+// and split the INPUTS: wave w loads, bit-slices and folds inputs
+// [w K/W, (w+1) K/W) into partial planes of all R rows; the partials meet in
+// LDS and wave w finishes rows [w R/W, (w+1) R/W) (the other waves' partials
+// XORed in, inverse transpose, stores). Same VALU as one wave per tile (each
+// input transposed and tabled once, each output transposed once) plus R/W x 8
+// XORs per partner wave, but W waves per 2 KiB of each share: a CU keeps
+// enough waves to overlap the folds with the loads while fewer bytes -- fewer
+// DRAM pages -- are in flight (one-wave tiles need 6 per
+// CU, 16 shares x 2 KiB each in flight, and stream below the 4 KiB-per-
+// workgroup probe shape).
+// LDS per column group: [owner wave d][partner q (W-1)][row of d (R/W)][2 halves][64 lanes] x 16 B.
+constexpr unsigned ksplit_lds_bytes(int C, int W, int R) {
+  return W > 1 ? static_cast<unsigned>(C * W * (W - 1) * (R / W) * 2 * 64 * 16) : 16u;
+}
+template <int C, int W, int R>
+struct KsplitLds {
+  v4 v[ksplit_lds_bytes(C, W, R) / 16];
+};
+
+template <class M, int W, int G, int WI>
+__device__ __forceinline__ void bs_ksplit_wave(const ApplyArgs &a, uint32_t stripe, uint32_t v0,
+                                               uint32_t cols, uint32_t lane, v4 *lds) {
+  constexpr int K = M::K, R = M::R, KW = K / W, RW = R / W, J0 = WI * KW;
+  static_assert(K % W == 0 && R % W == 0 && KW % G == 0, "input split: W | k, W | r, G | k / W");
+  uint32_t acc[R][8];
+#pragma unroll
+  for (int p = 0; p < R; p++)
+#pragma unroll
+    for (int b = 0; b < 8; b++) acc[p][b] = 0;
+
+  v4 buf[2][G][2];
+  const uint32_t ca = v0 < cols ? v0 : cols - 1, cb = v0 + 64 < cols ? v0 + 64 : cols - 1;
+  load_group<G>(a, J0, stripe, ca, cb, buf[0]);
+  static_for<KW / G>([&](auto GI) {
+    constexpr int gi = decltype(GI)::value;
+    if constexpr (gi + 1 < KW / G)
+      load_group<G>(a, J0 + (gi + 1) * G, stripe, ca, cb, buf[(gi + 1) & 1]);
+    static_for<G>([&](auto GG) {
+      constexpr int g = decltype(GG)::value;
+      constexpr int j = J0 + gi * G + g;
+      const v4 &A = buf[gi & 1][g][0], &Bv = buf[gi & 1][g][1];
+      if constexpr (((M::copy_mask >> j) & 1ull) != 0) {
+        v4 *c = reinterpret_cast<v4 *>(a.copy[j] + static_cast<uint64_t>(stripe) * a.copy_stride[j]);
+        if (v0 < cols) st_nt(c + v0, A);
+        if (v0 + 64 < cols) st_nt(c + v0 + 64, Bv);
+      }
+      uint32_t x[8] = {A[0], A[1], A[2], A[3], Bv[0], Bv[1], Bv[2], Bv[3]};
+      asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                   "+v"(x[6]), "+v"(x[7]));
+      transpose8(x);
+      fold_planes<M, j>(acc, x);
+      fence_acc(acc);
+    });
+  });
+
+  if constexpr (W > 1) {
+    // the partials of the rows the other waves own
+    static_for<W>([&](auto DI) {
+      constexpr int d = decltype(DI)::value;
+      if constexpr (d != WI) {
+        constexpr int q = WI < d ? WI : WI - 1;
+        static_for<RW>([&](auto RR) {
+          constexpr int rr = decltype(RR)::value, p = d * RW + rr;
+          v4 *slot = lds + (((d * (W - 1) + q) * RW + rr) * 2) * 64 + lane;
+          slot[0] = v4{acc[p][0], acc[p][1], acc[p][2], acc[p][3]};
+          slot[64] = v4{acc[p][4], acc[p][5], acc[p][6], acc[p][7]};
+        });
+      }
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    static_for<W - 1>([&](auto QI) {
+      constexpr int q = decltype(QI)::value;
+      static_for<RW>([&](auto RR) {
+        constexpr int rr = decltype(RR)::value, p = WI * RW + rr;
+        const v4 *slot = lds + (((WI * (W - 1) + q) * RW + rr) * 2) * 64 + lane;
+        const v4 P = slot[0], Q = slot[64];
+        acc[p][0] ^= P[0];
+        acc[p][1] ^= P[1];
+        acc[p][2] ^= P[2];
+        acc[p][3] ^= P[3];
+        acc[p][4] ^= Q[0];
+        acc[p][5] ^= Q[1];
+        acc[p][6] ^= Q[2];
+        acc[p][7] ^= Q[3];
+      });
+    });
+  }
+  static_for<RW>([&](auto RR) {
+    constexpr int p = WI * RW + decltype(RR)::value;
+    transpose8(acc[p]);
+    v4 *q = reinterpret_cast<v4 *>(a.out[p] + static_cast<uint64_t>(stripe) * a.out_stride[p]);
+    const v4 A = {acc[p][0], acc[p][1], acc[p][2], acc[p][3]};
+    const v4 Bv = {acc[p][4], acc[p][5], acc[p][6], acc[p][7]};
+    if (v0 < cols) st_nt(q + v0, A);
+    if (v0 + 64 < cols) st_nt(q + v0 + 64, Bv);
+  });
+}
+
+// Grid: nstripes x tiles of C x 128 16-B columns, 64 C W lanes (wave i:
+// column group i / W, input part i % W).
+template <class M, int C, int W, int G, int SWZ = 0>
+__device__ __forceinline__ void bs_ksplit_body(const ApplyArgs &a) {
+  __shared__ KsplitLds<C, W, M::R> lds;
+  constexpr uint32_t CPT = 128 * C;
+  const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
+  const uint32_t tps = (cols + CPT - 1) / CPT;
+  const uint32_t stripe = blockIdx.x / tps;
+  uint32_t tile = blockIdx.x - stripe * tps;
+  if constexpr (SWZ == 1) tile = (tile + stripe * (tps / 8 + 1)) % tps;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t cg = wid / W, w = wid - cg * W;
+  const uint32_t v0 = tile * CPT + cg * 128 + lane;
+  v4 *mine = lds.v + cg * (ksplit_lds_bytes(1, W, M::R) / 16);
+  static_for<W>([&](auto WI) {
+    constexpr int wi = decltype(WI)::value;
+    if (w == wi) bs_ksplit_wave<M, W, G, wi>(a, stripe, v0, cols, lane, mine);
+  });
+}
+
 template <class M, int G, int T = kBsThreads, int SWZ = 0>
 __device__ __forceinline__ void bs_kernel_body(const ApplyArgs &a) {
   constexpr uint32_t CPT = bs_cols_per_tile(T);

@@ -119,7 +119,10 @@ static hipError_t release_table(storb_rs_ctx *ctx, Tables *t, hipStream_t live) 
   }
   // a last use on a stream this call does not hold, not yet marked (rare:
   // the caller moved to other streams right after it)
-  if (e == hipSuccess && sync) e = hipDeviceSynchronize();
+  if (e == hipSuccess && sync) {
+    ctx->n_device_syncs++;
+    e = hipDeviceSynchronize();
+  }
   if (e == hipSuccess) e = hipFreeAsync(t->dev, ctx->stream);
   if (e == hipSuccess) t->dev = nullptr;
   return e;
@@ -135,6 +138,7 @@ static int evict_tables(storb_rs_ctx *ctx, hipStream_t live) {
   // oldest work on `home` this table has, long finished in practice.
   HIP_TRY(ctx, hipEventSynchronize(t->uploaded));
   ctx->tables.erase(victim);  // events are released once they complete
+  ctx->n_tables = ctx->tables.size();
   return STORB_RS_OK;
 }
 
@@ -304,6 +308,7 @@ int get_tables(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef
   t->tick = ++ctx->table_tick;
   *out = t.get();
   ctx->tables.emplace(std::move(key), std::move(t));
+  ctx->n_tables = ctx->tables.size();
   return STORB_RS_OK;
 }
 
@@ -724,6 +729,8 @@ int storb_rs_ctx_create(int device_ordinal, storb_rs_ctx **out) {
   if (!g.ok) return STORB_RS_ENODEV;
   auto *c = new storb_rs_ctx();
   c->device = dev;
+  c->create_node = cpu_numa_node(sched_getcpu());
+  c->device_node = storb_rs_device_numa_node(dev);
   c->zc_max = 64ull << 20;
   if (const char *e = std::getenv("STORB_RS_ZC_MAX")) c->zc_max = std::strtoull(e, nullptr, 10);
   if (const char *e = std::getenv("STORB_RS_ZC_BATCH")) c->zc_batch = std::atoi(e) != 0;
@@ -842,9 +849,10 @@ int storb_rs_ctx_stats(const storb_rs_ctx *ctx, storb_rs_ctx_stats_t *out) {
     std::lock_guard<std::mutex> lk(c->async_mu);
     out->live_ops = c->live_ops.size();
   }
-  // the table cache changes under ctx->mu (every call that launches holds it)
-  std::lock_guard<std::mutex> lk(c->mu);
-  out->tables = ctx->tables.size();
+  out->tables = ctx->n_tables.load();  // no lock: a monitor must not wait on a batch call
+  out->device_syncs = ctx->n_device_syncs.load();
+  out->caller_node = ctx->create_node;
+  out->device_node = ctx->device_node;
   return STORB_RS_OK;
 }
 

@@ -32,8 +32,8 @@ def test_jit_blocks_match_row_split_and_row_blocks():
             else:
                 nb = -(-rows // 16)
                 want = (nb, rows // nb)
-            assert bench.jit_blocks(k, rows) == want, (k, rows)
-    assert bench.jit_blocks(41, 20) == (2, 10)
+            assert bench.prof.jit_blocks(k, rows) == want, (k, rows)
+    assert bench.prof.jit_blocks(41, 20) == (2, 10)
 
 
 def test_line_extras_cpu_baseline_on_every_rank0_line():
@@ -68,3 +68,57 @@ def test_force_pg_flag_parses():
     a = bench.parse(["--force-pg", "--dist-backend", "nccl"])
     assert a.force_pg and a.dist_backend == "nccl"
     assert not bench.parse([]).force_pg
+
+
+def test_all_rank_host_leg_policy():
+    """the concurrent host-inclusive leg runs on EVERY
+    rank at every world size for the host-bound geometries (the driver's
+    1/2/4/8-GPU lines carry it), never in the PMC child runs."""
+    bench = load_bench()
+    for config in (2, 5, 6):
+        assert bench.all_rank_leg(False, config, False)
+        assert not bench.all_rank_leg(True, config, False)   # --minimal
+        assert not bench.all_rank_leg(False, config, True)   # --no-host-path
+    for config in (3, 4, 7):
+        assert not bench.all_rank_leg(False, config, False)
+    a = bench.parse([])
+    assert a.pin == "numa" and a.host_mib == 256
+
+
+def test_aggregate_all_ranks_is_sum_over_slowest():
+    from benchkit import GIB, host
+    recs = []
+    for r, slow in ((0, 1.0), (1, 2.0)):
+        geo = {}
+        for name, chunk in host.ALL_RANK_GEOMETRIES:
+            row = {"k": 4, "m_total": 6, "chunk_bytes": chunk, "chunks": 4, "lost": [0, 1],
+                   "reps": 2, "bytes_per_rep": 4 * chunk, "roundtrip_pageable": True,
+                   "roundtrip_pinned": True, "parity_modes_agree": True,
+                   "parity_sha256": f"d{r}"}
+            for leg in ("encode_pageable", "encode_pinned", "decode_pageable", "decode_pinned"):
+                row[f"{leg}_s"] = slow
+            geo[name] = row
+        recs.append({"rank": r, "device": 0, "geometries": geo})
+    pins = [{"gpu_numa_node": 0, "cpus": "0-7", "pinned": True}] * 2
+    out = host.aggregate_all_ranks(recs, pins)
+    assert out["ranks"] == 2
+    for name, chunk in host.ALL_RANK_GEOMETRIES:
+        g = out["geometries"][name]
+        want = 2 * (2 * 4 * chunk) / GIB / 2.0
+        assert abs(g["encode_pageable"]["aggregate_GiBps"] - round(want, 3)) < 1e-9
+        assert g["encode_pageable"]["per_rank_GiBps"][0] == 2 * g["encode_pageable"]["per_rank_GiBps"][1]
+        assert g["bit_exact"] and g["parity_sha256_per_rank"] == ["d0", "d1"]
+    assert [p["cpus"] for p in out["per_rank"]] == ["0-7", "0-7"]
+
+
+def test_cpu_ranges_and_pin_without_gpu():
+    from benchkit import cpu
+    assert cpu.cpu_ranges([0, 1, 2, 5, 7, 8]) == "0-2,5,7-8"
+    assert cpu.cpu_ranges([]) == ""
+    saved = os.sched_getaffinity(0)
+    info = cpu.pin_rank(0, "numa")  # no GPU here: node unknown, nothing pinned
+    assert info["gpu_numa_node"] == -1 and not info["pinned"]
+    assert os.sched_getaffinity(0) == saved
+    with cpu.affinity(sorted(saved)[:1]):
+        assert os.sched_getaffinity(0) == set(sorted(saved)[:1])
+    assert os.sched_getaffinity(0) == saved

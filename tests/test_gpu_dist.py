@@ -100,11 +100,17 @@ def test_two_rank_processes_encode_on_the_gpu_vs_oracle():
 def test_bench_two_ranks_spawned_on_one_gpu():
     """bench.py --gpus 2 as the driver would start it at N = 2, except that
     both ranks share the box's one GPU (STORB_BENCH_DEVICE=0, gloo): the line
-    says 2 ranks ran and carries both ranks' GPU time."""
+    says 2 ranks ran and carries both ranks' GPU time, each rank's CPU set and
+    GPU NUMA node, and the concurrent all-rank host-inclusive leg (VERDICT r5
+    item 1) -- whose per-rank parity digests are recomputed here with the
+    oracle from the same seeds (SEED_BASE + global chunk index)."""
+    from oracle import coracle
     env = dict(os.environ, STORB_BENCH_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    mib = 16
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--steps", "5", "--warmup", "1", "--dist-backend", "gloo",
-                        "--chunks", "64", "--cpu-seconds", "0.2", "--settle-ms", "0"],
+                        "--chunks", "64", "--cpu-seconds", "0.2", "--settle-ms", "0",
+                        "--host-mib", str(mib)],
                        env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
@@ -112,4 +118,20 @@ def test_bench_two_ranks_spawned_on_one_gpu():
     assert line["launch"]["pg_ranks"] == 2 and line["launch"]["backend"] == "gloo"
     assert len(line["per_rank"]) == 2
     assert all(x["gpu_ms_per_step"] > 0 for x in line["per_rank"])
+    assert all(x["cpus"] and "gpu_numa_node" in x for x in line["per_rank"])
     assert line["value"] > 0
+    hl = line["pcie_inclusive_all_ranks"]
+    assert hl["ranks"] == 2 and len(hl["per_rank"]) == 2
+    assert all(p["cpus"] and p["gpu_numa_node"] is not None for p in hl["per_rank"])
+    for name, g in hl["geometries"].items():
+        assert g["bit_exact"], name
+        for leg in ("encode_pageable", "encode_pinned", "decode_pageable", "decode_pinned"):
+            assert g[leg]["aggregate_GiBps"] > 0 and len(g[leg]["per_rank_GiBps"]) == 2
+        k, n, chunk, nch = g["k"], g["m_total"], g["chunk_bytes"], g["chunks"]
+        assert nch == max(1, (mib << 20) // chunk)
+        for rank in range(2):
+            h = hashlib.sha256()
+            for c in range(nch):
+                data = coracle.splitmix_bytes(0x5709B + rank * nch + c, chunk)
+                h.update(np.ascontiguousarray(coracle.encode(k, n, data)[0][k:]).tobytes())
+            assert g["parity_sha256_per_rank"][rank] == h.hexdigest(), (name, rank)

@@ -309,3 +309,36 @@ def test_descriptor_slots_reused_across_streams(ctx):
     ref = torch.from_numpy(data.reshape(-1).copy()).to(DEV)
     for i, out in enumerate(outs):
         assert torch.equal(out, ref), (i, plan[i])
+
+
+def test_alternating_caller_streams_take_no_device_syncs(ctx):
+    """the stream-ordering fallbacks (a table's or a descriptor
+    slot's last use on a stream no order mark covers) synchronise the whole
+    device; they are counted (storb_rs_ctx_stats device_syncs) and must stay
+    rare for a caller that alternates between its own streams, as Storb's
+    download tasks would. Also the context reports where it was created and
+    where its GPU hangs (caller_node / device_node)."""
+    k, n, B, ns = 4, 6, 64 << 10, 64
+    data, par = oracle_stripes(k, n, B, ns, 5151)
+    sets = download_sets(k, n, ns, 5252)
+    dd = torch.from_numpy(data.reshape(-1).copy()).to(DEV)
+    dp = torch.from_numpy(par.reshape(-1).copy()).to(DEV)
+    a, b = torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV)
+    before = ctx.stats()["device_syncs"]
+    outs = [torch.zeros_like(dd) for _ in range(64)]
+    torch.cuda.synchronize()
+    for i, out in enumerate(outs):
+        s = (a if i % 2 == 0 else b).cuda_stream
+        ctx.decode_stripes_dev(k, n, B, sets, dd.data_ptr(), dp.data_ptr(), out.data_ptr(),
+                               stream=s)
+        # a new matrix now and then on the other stream: the table cache
+        ctx.decode_batch_dev(k, n, B, ns, [i % 3, 3, 4, 5], dd.data_ptr(), dp.data_ptr(),
+                             out.data_ptr(), stream=(b if i % 2 == 0 else a).cuda_stream)
+    torch.cuda.synchronize()
+    ref = torch.from_numpy(data.reshape(-1).copy()).to(DEV)
+    for out in outs:
+        assert torch.equal(out, ref)
+    st = ctx.stats()
+    assert st["device_syncs"] - before <= 2, st
+    assert st["device_node"] == _lib.device_numa_node(0)
+    assert st["caller_node"] >= -1

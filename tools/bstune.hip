@@ -48,6 +48,61 @@ __global__ __launch_bounds__(T) void k_bs(const ApplyArgs a) {
   bs::bs_kernel_body<bs::EncMat<K, N>, G, T, SWZ>(a);
 }
 
+template <int K, int N, int C, int W, int G, int SWZ>
+__global__ __launch_bounds__(64 * C * W) void k_ks(const ApplyArgs a) {
+  bs::bs_ksplit_body<bs::EncMat<K, N>, C, W, G, SWZ>(a);
+}
+
+// The access structure with (almost) no GF work: row 0 = XOR of the
+// bit-sliced inputs (transposes kept), rows 1.. zero (stored). What a launch
+// shape streams at when the folds cost nothing (BSTUNE_NOGF).
+template <int K_, int N_>
+struct ZeroMat {
+  static constexpr int K = K_, R = N_ - K_;
+  static constexpr unsigned long long copy_mask = 0;
+  struct Net {
+    unsigned char row[R][K][8];
+  };
+  static constexpr Net make() {
+    Net n{};
+    for (int j = 0; j < K; j++)
+      for (int b = 0; b < 8; b++) n.row[0][j][b] = static_cast<unsigned char>(1u << b);
+    return n;
+  }
+  static constexpr Net net = make();
+};
+
+template <int K, int N, int G, int T, int SWZ>
+__global__ __launch_bounds__(T) void k_bs0(const ApplyArgs a) {
+  bs::bs_kernel_body<ZeroMat<K, N>, G, T, SWZ>(a);
+}
+
+template <int K, int N, int C, int W, int G, int SWZ>
+__global__ __launch_bounds__(64 * C * W) void k_ks0(const ApplyArgs a) {
+  bs::bs_ksplit_body<ZeroMat<K, N>, C, W, G, SWZ>(a);
+}
+
+// 16 B per lane, every input loaded up front (the round-2 probe shape).
+template <int K, int R, int T>
+__global__ __launch_bounds__(T) void k_flat(const ApplyArgs a) {
+  const uint32_t cols = static_cast<uint32_t>(a.block >> 4), tps = cols / T;
+  const uint32_t stripe = blockIdx.x / tps, t = blockIdx.x - stripe * tps;
+  const uint32_t c = t * T + threadIdx.x;
+  bs::v4 v[K];
+#pragma unroll
+  for (int j = 0; j < K; j++)
+    v[j] = bs::ld_nt(reinterpret_cast<const bs::v4 *>(a.in[j] + (uint64_t)stripe * a.in_stride[j]) + c);
+  bs::v4 acc = v[0];
+#pragma unroll
+  for (int j = 1; j < K; j++) acc ^= v[j];
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    bs::v4 o = acc;
+    o.x ^= i;
+    bs::st_nt(reinterpret_cast<bs::v4 *>(a.out[i] + (uint64_t)stripe * a.out_stride[i]) + c, o);
+  }
+}
+
 using Fn = std::function<hipError_t(const ApplyArgs &, hipStream_t)>;
 struct V {
   std::string name;
@@ -69,6 +124,55 @@ void add(std::vector<V> &vs, std::initializer_list<int> caps) {
                   }, {}});
 }
 
+// Input-split workgroups (rs_bitslice_core.h bs_ksplit_body): W waves on the
+// same 2 KiB of every share, each folding k / W inputs, G per load group.
+template <int K, int N, int C, int W, int G, int SWZ>
+void add_ks(std::vector<V> &vs, std::initializer_list<int> caps) {
+  for (int cap : caps)
+    vs.push_back({"ksplit C=" + std::to_string(C) + " W=" + std::to_string(W) + " G=" +
+                      std::to_string(G) + " swz=" + std::to_string(SWZ) + " cap=" +
+                      std::to_string(cap),
+                  [cap](const ApplyArgs &a, hipStream_t s) {
+                    const uint64_t cpt = 128 * C;
+                    const uint64_t blocks = ((a.block / 16 + cpt - 1) / cpt) * a.nstripes;
+                    return launch_lds<k_ks<K, N, C, W, G, SWZ>>(
+                        blocks, 64 * C * W, cap_lds(cap, bs::ksplit_lds_bytes(C, W, N - K)), s, a);
+                  }, {}});
+}
+
+template <int K, int N, int G, int T, int SWZ>
+void add0(std::vector<V> &vs, std::initializer_list<int> caps) {
+  for (int cap : caps)
+    vs.push_back({"nogf G=" + std::to_string(G) + " T=" + std::to_string(T) + " swz=" +
+                      std::to_string(SWZ) + " cap=" + std::to_string(cap),
+                  [cap](const ApplyArgs &a, hipStream_t s) {
+                    const uint64_t cpt = bs::bs_cols_per_tile(T);
+                    const uint64_t blocks = ((a.block / 16 + cpt - 1) / cpt) * a.nstripes;
+                    return launch_lds<k_bs0<K, N, G, T, SWZ>>(blocks, T, cap_lds(cap, 0), s, a);
+                  }, {}});
+}
+template <int K, int N, int C, int W, int G, int SWZ>
+void add_ks0(std::vector<V> &vs, std::initializer_list<int> caps) {
+  for (int cap : caps)
+    vs.push_back({"nogf ksplit C=" + std::to_string(C) + " W=" + std::to_string(W) + " G=" +
+                      std::to_string(G) + " cap=" + std::to_string(cap),
+                  [cap](const ApplyArgs &a, hipStream_t s) {
+                    const uint64_t cpt = 128 * C;
+                    const uint64_t blocks = ((a.block / 16 + cpt - 1) / cpt) * a.nstripes;
+                    return launch_lds<k_ks0<K, N, C, W, G, SWZ>>(
+                        blocks, 64 * C * W, cap_lds(cap, bs::ksplit_lds_bytes(C, W, N - K)), s, a);
+                  }, {}});
+}
+template <int K, int N, int T>
+void add_flat(std::vector<V> &vs, std::initializer_list<int> caps) {
+  for (int cap : caps)
+    vs.push_back({"flat16B T=" + std::to_string(T) + " cap=" + std::to_string(cap),
+                  [cap](const ApplyArgs &a, hipStream_t s) {
+                    const uint64_t blocks = (a.block / 16 / T) * a.nstripes;
+                    return launch_lds<k_flat<K, N - K, T>>(blocks, T, cap_lds(cap, 0), s, a);
+                  }, {}});
+}
+
 // dec = false: encode layout (k data shares in, n - k parity shares out, each
 // region packed per stripe). dec = true: the in-place decode layout of
 // bench.py --erase R (data shares 0..R-1 lost, rebuilt into their slots of the
@@ -78,12 +182,26 @@ template <int K, int N>
 void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec = false) {
   constexpr int R = N - K;
   std::vector<V> vs;
-  if (!dec)
+  const bool nogf = std::getenv("BSTUNE_NOGF") != nullptr;
+  if (!dec && !nogf)
     vs.push_back({"product", [](const ApplyArgs &a, hipStream_t s) {
                     return bs::launch_bitslice<K, N>(a, s);
                   }, {}});
   constexpr int G = bs::bs_group(K, R);
-  if (std::getenv("BSTUNE_FEWROWS")) {  // decodes with few lost rows: G x (T, cap)
+  if (nogf) {  // access-shape ceilings; not compared bit-exactly across shapes
+    add0<K, N, G, 64, 1>(vs, {4, 6});
+    if constexpr (R == 8) {
+      add_ks0<K, N, 1, 4, 4, 1>(vs, {4, 6});
+      add_ks0<K, N, 2, 2, 8, 1>(vs, {2, 3});
+      add_ks0<K, N, 2, 2, 4, 1>(vs, {2, 3});
+      add_ks0<K, N, 2, 4, 4, 1>(vs, {1});
+    } else if constexpr (R == 16) {
+      add_ks0<K, N, 2, 2, 2, 1>(vs, {2, 3});
+    }
+    add_flat<K, N, 256>(vs, {0, 1, 2});
+    add_flat<K, N, 512>(vs, {1});
+    add_flat<K, N, 128>(vs, {2, 4});
+  } else if (std::getenv("BSTUNE_FEWROWS")) {  // decodes with few lost rows: G x (T, cap)
     if constexpr (R <= 8) {
       add<K, N, 2, 128, 0>(vs, {3});
       add<K, N, 4, 128, 0>(vs, {3});
@@ -92,6 +210,30 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec =
       add<K, N, 4, 64, 0>(vs, {5});
       add<K, N, 4, 128, 1>(vs, {3});
     }
+  } else if (std::getenv("BSTUNE_KSPLIT")) {  // input-split workgroups x cap
+    if constexpr (R == 8) {
+      add_ks<K, N, 2, 2, 8, 1>(vs, {1, 2, 3});
+      add_ks<K, N, 2, 2, 4, 1>(vs, {1, 2, 3});
+      add_ks<K, N, 2, 2, 8, 0>(vs, {2});
+      add_ks<K, N, 1, 4, 4, 1>(vs, {2, 4});
+      add_ks<K, N, 1, 2, 8, 1>(vs, {4});
+    }
+    if constexpr (R == 16) {
+      add<K, N, G, 128, 0>(vs, {2, 3, 4});
+      add_ks<K, N, 2, 2, 2, 1>(vs, {1, 2});
+      add_ks<K, N, 2, 2, 4, 1>(vs, {1, 2});
+      add_ks<K, N, 2, 2, 8, 1>(vs, {1, 2});
+      add_ks<K, N, 1, 2, 4, 1>(vs, {2, 4});
+    }
+  } else if (std::getenv("BSTUNE_LOWCAP")) {  // fewer bytes in flight per CU
+    add<K, N, G, 64, 1>(vs, {2, 3, 4, 6});
+    add<K, N, G, 128, 1>(vs, {1, 2, 3});
+    add<K, N, G, 256, 1>(vs, {1});
+    if constexpr (K % 4 == 0 && G != 4) {
+      add<K, N, 4, 64, 1>(vs, {3, 4, 6, 8});
+      add<K, N, 4, 128, 1>(vs, {2, 3});
+    }
+    if constexpr (K % 2 == 0 && G != 2) add<K, N, 2, 64, 1>(vs, {4, 6, 8});
   } else if (std::getenv("BSTUNE_GROUPS")) {  // load-group size at the product shapes
     add<K, N, G, 64, 1>(vs, {6});
     add<K, N, G, 128, 0>(vs, {3, 4});
@@ -142,7 +284,7 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec =
     CK(vs[vi].fn(a, s));
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(vi ? got.data() : ref.data(), res, res_bytes, hipMemcpyDeviceToHost));
-    if (vi && std::memcmp(got.data(), ref.data(), res_bytes)) {
+    if (vi && !nogf && std::memcmp(got.data(), ref.data(), res_bytes)) {
       std::printf("MISMATCH %s %s\n", name, vs[vi].name.c_str());
       std::exit(2);
     }
@@ -163,7 +305,8 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec =
       v.us.push_back(ms * 1000.f / reps);
     }
   const double bytes = (double)in_bytes + out_bytes;  // k*B read + r*B written, either layout
-  std::printf("%s: %.3f GB algorithmic per launch, every variant bit-exact\n", name, bytes / 1e9);
+  std::printf("%s: %.3f GB algorithmic per launch%s\n", name, bytes / 1e9,
+              nogf ? " (no-GF shapes: outputs not compared)" : ", every variant bit-exact");
   for (auto &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
