@@ -48,6 +48,8 @@ def lib():
         L.zo_piece_length.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
         L.zo_get_k_and_m.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.zo_splitmix_fill.argtypes = [C.c_uint64, C.c_void_p, C.c_size_t]
+        L.zo_decode_many.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_void_p, C.c_size_t,
+                                     C.c_uint, C.c_void_p, C.c_void_p, C.c_int]
         L.zo_encode_many.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_size_t, C.c_uint,
                                      C.c_void_p, C.c_int]
         L.zo_bench_roundtrip.argtypes = [C.c_uint, C.c_uint, C.c_void_p, C.c_size_t, C.c_uint,
@@ -91,6 +93,22 @@ def encode_parity_many(k: int, n: int, data: np.ndarray, chunk_len: int, nchunks
     rc = lib().zo_encode_many(k, n, _ptr(data), chunk_len, nchunks, _ptr(out), threads)
     if rc != 0:
         raise ValueError("zo_encode_many failed")
+    return out
+
+
+def decode_many(k: int, n: int, data: np.ndarray, parity: np.ndarray, block: int,
+                nchunks: int, survivors, threads: int = 1) -> np.ndarray:
+    """Whole-batch decode (zo_decode_many): chunk c rebuilt from the survivors
+    (sorted, k of them) among its data shares (data, k*block per chunk) and
+    parity shares (parity, (n-k)*block per chunk); returns nchunks*k*block."""
+    surv = sorted(survivors)[:k]
+    sv = (C.c_uint * k)(*surv)
+    out = np.zeros(nchunks * k * block, dtype=np.uint8)
+    rc = lib().zo_decode_many(k, n, _ptr(np.ascontiguousarray(data)),
+                              _ptr(np.ascontiguousarray(parity)), block, nchunks, sv,
+                              _ptr(out), threads)
+    if rc != 0:
+        raise ValueError(f"zo_decode_many failed ({rc})")
     return out
 
 

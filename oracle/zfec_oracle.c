@@ -460,6 +460,61 @@ int zo_encode_many(unsigned k, unsigned n, const uint8_t *data, size_t len,
   return 0;
 }
 
+/* ------------------------------------------------- threaded batch decode */
+typedef struct {
+  unsigned k, n, first, last;
+  const uint8_t *data, *parity;
+  size_t block;
+  const unsigned *surv;
+  uint8_t *out;
+  int bad;
+} dec_job;
+
+static void *dec_worker(void *arg) {
+  dec_job *j = (dec_job *)arg;
+  const size_t B = j->block, p = j->n - j->k;
+  const uint8_t **sv = malloc(sizeof(uint8_t *) * j->k);
+  for (unsigned c = j->first; c < j->last; c++) {
+    for (unsigned i = 0; i < j->k; i++) {
+      const unsigned s = j->surv[i];
+      sv[i] = s < j->k ? j->data + ((size_t)c * j->k + s) * B
+                       : j->parity + ((size_t)c * p + (s - j->k)) * B;
+    }
+    if (zo_decode_impl(j->k, j->n, sv, j->surv, j->k, B, 0, j->out + (size_t)c * j->k * B,
+                       NULL) != 0)
+      j->bad++;
+  }
+  free(sv);
+  return NULL;
+}
+
+int zo_decode_many(unsigned k, unsigned n, const uint8_t *data, const uint8_t *parity,
+                   size_t block, unsigned nchunks, const unsigned *surv, uint8_t *out,
+                   int threads) {
+  zo_init();
+  if (k < 1 || n > 256 || k > n || block == 0 || nchunks == 0) return -1;
+  if (threads <= 0) threads = 1;
+  if ((unsigned)threads > nchunks) threads = (int)nchunks;
+  pthread_t *tid = malloc(sizeof(pthread_t) * threads);
+  dec_job *jobs = malloc(sizeof(dec_job) * threads);
+  const unsigned per = (nchunks + threads - 1) / threads;
+  for (int t = 0; t < threads; t++) {
+    dec_job jb = {k, n, t * per < nchunks ? t * per : nchunks,
+                  (t + 1) * per < nchunks ? (t + 1) * per : nchunks,
+                  data, parity, block, surv, out, 0};
+    jobs[t] = jb;
+    pthread_create(&tid[t], NULL, dec_worker, &jobs[t]);
+  }
+  int bad = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(tid[t], NULL);
+    bad += jobs[t].bad;
+  }
+  free(tid);
+  free(jobs);
+  return bad;
+}
+
 /* ----------------------------------------------- threaded round trips */
 typedef struct {
   unsigned k, n, first, last, nerased;

@@ -116,6 +116,15 @@ void zo_splitmix_fill(uint64_t seed, uint8_t *out, size_t len);
 int zo_encode_many(unsigned k, unsigned n, const uint8_t *data, size_t len,
                    unsigned nchunks, uint8_t *parity, int threads);
 
+/* Multi-threaded batch decode (test checker for whole device batches):
+ * chunk c's data share i < k at data + (c*k + i)*block, parity share i >= k
+ * at parity + (c*(n-k) + i-k)*block; the k survivors surv[] (sorted) rebuild
+ * chunk c (padlen 0) into out + c*k*block. Returns the number of chunks
+ * that failed (0 = all rebuilt), -1 on bad input. */
+int zo_decode_many(unsigned k, unsigned n, const uint8_t *data, const uint8_t *parity,
+                   size_t block, unsigned nchunks, const unsigned *surv, uint8_t *out,
+                   int threads);
+
 /* Multi-threaded encode + decode round trips of nchunks independent chunks
  * of len bytes (data back to back), losing the `nerased` shares listed in
  * erased[] (first k survivors by index decode). Returns the number of

@@ -249,17 +249,19 @@ __device__ __forceinline__ void copy_group(const V &v, uint32_t k, uint32_t cols
   }
 }
 
+// The folds of one tile: acc[i] = XOR_j M[i][j] * in_j over the tile's
+// column(s), for the k <= KM inputs of view v (perm_tile stores them; the
+// input-split descriptor tiles reduce several waves' acc first).
 template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD,
           bool COPY = false, class V, class TP>
-__device__ __forceinline__ void perm_tile(const V &v, TP tabs, uint32_t k,
-                                          uint32_t r, uint32_t cols, uint32_t c0) {
+__device__ __forceinline__ void perm_acc(const V &v, TP tabs, uint32_t k, uint32_t r,
+                                         uint32_t cols, uint32_t c0, u32x4 (&acc)[RM][U]) {
   // the groups cover the bucket's KM input slots (inputs >= k skipped): a G
   // that does not divide KM would drop the last KM % G inputs (a G = 12 A/B
   // build at k = 32 failed the bench's round-trip check, round 5)
   static_assert(KM % G == 0, "load group size must divide the k bucket");
   constexpr int NG = KM / G;
   u32x4 buf[2][G][U];
-  u32x4 acc[RM][U];
 #pragma unroll
   for (int i = 0; i < RM; i++)
 #pragma unroll
@@ -349,7 +351,14 @@ __device__ __forceinline__ void perm_tile(const V &v, TP tabs, uint32_t k,
       }
     }
   }
+}
 
+template <int KM, int RM, int T, int U, bool BAR, int G, bool PAIR, bool GUARD,
+          bool COPY = false, class V, class TP>
+__device__ __forceinline__ void perm_tile(const V &v, TP tabs, uint32_t k,
+                                          uint32_t r, uint32_t cols, uint32_t c0) {
+  u32x4 acc[RM][U];
+  perm_acc<KM, RM, T, U, BAR, G, PAIR, GUARD, COPY>(v, tabs, k, r, cols, c0, acc);
 #pragma unroll
   for (int i = 0; i < RM; i++) {
     if (i >= static_cast<int>(r)) continue;
@@ -579,6 +588,110 @@ __global__ __launch_bounds__(mix_threads<KM>()) void rs_apply_desc_mix(const Des
   if (r == 3) STORB_MIX_CASE(3)
   STORB_MIX_CASE(4)
 #undef STORB_MIX_CASE
+}
+
+// ------------------------------------------- input-split descriptor tiles
+// Inputs j0 .. of a view (one wave's part of an input-split tile).
+template <class V>
+struct OffsetView {
+  const V &v;
+  uint32_t j0;
+  __device__ __forceinline__ auto in(int j) const { return v.in(static_cast<int>(j0) + j); }
+  __device__ __forceinline__ auto out(int i) const { return v.out(i); }
+  __device__ __forceinline__ bool has_copy(int j) const { return v.has_copy(static_cast<int>(j0) + j); }
+  __device__ __forceinline__ auto copy(int j) const { return v.copy(static_cast<int>(j0) + j); }
+  __device__ __forceinline__ bool accumulate() const { return v.accumulate(); }
+};
+
+// The mixed-row descriptor launch with W waves per 64-column tile
+// (rs_apply_desc_mix_ks): the waves of a workgroup cover the SAME 1 KiB of
+// every share and split the k inputs (KM / W each); their partial rows meet
+// in LDS and wave w stores rows w, w + W, ... So a tile keeps the one-wave
+// tile's footprint (1 KiB of each share) with W waves to hide the v_perm
+// folds' latency: the access shape that streams best for k = 16 -- one-wave
+// tiles capped at 8 per CU, 0.794 of 8 TB/s with no GF work
+// (tools/dlprobe.hip, profiles/r5e_dlprobe.txt) -- needed more waves than
+// that cap leaves for the GF work (the uncapped product held 0.769).
+template <int KM, int W>
+struct MixKs {
+  static constexpr int T = 64 * W, KW = KM / W;
+  static_assert(KM % W == 0, "W must divide the k bucket");
+};
+
+template <int KM, int W, int R, bool GUARD>
+__device__ __forceinline__ void mix_ks_tile(const DescArgs &a, cu64 *rec, const PermTab *tabs,
+                                            uint32_t cols, uint32_t c0, u32x4 *red) {
+  using S = MixKs<KM, W>;
+  constexpr int KW = S::KW;
+  constexpr int G = KW < Tune<KM, R>::G ? KW : Tune<KM, R>::G;
+  constexpr bool PAIR = mix_pair<KM, R>() && G % 2 == 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t j0 = w * KW;
+  const uint32_t kw = a.k > j0 ? (a.k - j0 < KW ? a.k - j0 : KW) : 0u;
+  const DescView v{rec, a.k, a.r};
+  const OffsetView<DescView> ov{v, j0};
+  u32x4 acc[R][1];
+  perm_acc<KW, R, 64, 1, false, G, PAIR, GUARD, false>(ov, tabs + j0 * R, kw, R, cols, c0, acc);
+#pragma unroll
+  for (int i = 0; i < R; i++) red[(w * R + i) * 64 + lane] = acc[i][0];
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < R; i++) {
+    if (i % W != static_cast<int>(w)) continue;  // wave-uniform
+    u32x4 x = acc[i][0];
+#pragma unroll
+    for (int q = 0; q < W; q++)
+      if (q != static_cast<int>(w)) x ^= red[(q * R + i) * 64 + lane];
+    if (!GUARD || c0 < cols) st_stream(v.out(i) + c0, x);
+  }
+}
+
+template <int KM, int W>
+__global__ __launch_bounds__((MixKs<KM, W>::T)) void rs_apply_desc_mix_ks(const DescArgs a) {
+  __shared__ __attribute__((aligned(16))) PermTab lds_ptab[KM * kMixR];
+  __shared__ u32x4 red[W * kMixR * 64];
+  const uint32_t cols = static_cast<uint32_t>(a.block >> 4);
+  const uint32_t tps = (cols + 63) / 64;
+  const uint32_t item = blockIdx.x / tps;
+  const uint32_t base = (blockIdx.x - item * tps) * 64;
+  cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
+  const uint32_t r = static_cast<uint32_t>(rec[0] >> 32);
+  const uint32_t rb = r <= 1 ? 1 : r;  // rows of the item's tables ([input][rb])
+  typedef const PermTab __attribute__((address_space(4))) cPermTab;
+  typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
+  cPermTab *gt = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
+  const uint32_t n16 = a.k * rb * (sizeof(PermTab) / 16);
+  for (uint32_t t = threadIdx.x; t < n16; t += MixKs<KM, W>::T)
+    reinterpret_cast<u32x4 *>(lds_ptab)[t] = ((gcu32x4 *)(gt))[t];
+  __syncthreads();
+  const uint32_t c0 = base + (threadIdx.x & 63);
+  const bool full = base + 64 <= cols;
+#define STORB_MIXKS_CASE(R)                                                          \
+  {                                                                                  \
+    if (full)                                                                        \
+      mix_ks_tile<KM, W, R, false>(a, rec, lds_ptab, cols, c0, red);                 \
+    else                                                                             \
+      mix_ks_tile<KM, W, R, true>(a, rec, lds_ptab, cols, c0, red);                  \
+    return;                                                                          \
+  }
+  if (r <= 1) STORB_MIXKS_CASE(1)
+  if (r == 2) STORB_MIXKS_CASE(2)
+  if (r == 3) STORB_MIXKS_CASE(3)
+  STORB_MIXKS_CASE(4)
+#undef STORB_MIXKS_CASE
+}
+
+template <int KM, int W>
+hipError_t launch_desc_mix_ks(const DescArgs &a, hipStream_t s, int cap) {
+  const uint64_t tps = ((a.block >> 4) + 63) / 64;
+  if (a.tpw != 1 || a.copy) return hipErrorInvalidConfiguration;
+  const uint64_t blocks = tps * a.nitems;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 0x7FFFFFFFull) return hipErrorInvalidConfiguration;
+  constexpr size_t stat = sizeof(PermTab) * KM * kMixR + sizeof(u32x4) * W * kMixR * 64;
+  return launch_lds<rs_apply_desc_mix_ks<KM, W>>(blocks, MixKs<KM, W>::T, cap_lds(cap, stat), s,
+                                                 a);
 }
 
 // The streamed single call's kernel (StreamArgs, rs_args.h): the table

@@ -291,3 +291,25 @@ def test_named_assumption_fixtures(golden):
         order = v["decode"].get("given_order", v["decode"].get("survivors"))
         rec = co.decode(k, n, [shares[i] for i in order], order, B, pad)
         assert sha(rec) == v["decode"]["data_sha256"] == sha(d), v["name"]
+
+
+def test_decode_many_rebuilds_every_chunk():
+    """The whole-batch oracle decode the BASELINE-size GPU tests check with
+    (tests/batch_oracle.py): encode_parity_many then decode_many from data
+    survivors and parity, for the config-3 erasure and a parity-only set."""
+    import batch_oracle as BO
+    for k, n, L, N, lost in ((8, 12, 4096, 6, (0, 3, 5)), (4, 6, 1024, 5, (9,)),
+                             (16, 24, 2048, 3, tuple(range(8)))):
+        B = L // k
+        data = BO.splitmix_chunks(11, L, N)
+        par = BO.parity_all(k, n, data, L, N)
+        for i in range(N):
+            want = co.encode(k, n, data[i * L:(i + 1) * L])[0][k:]
+            assert np.array_equal(par[i * (n - k) * B:(i + 1) * (n - k) * B].reshape(n - k, B), want)
+        surv = [i for i in range(n) if i not in lost][:k]
+        wiped = data.copy().reshape(N, k, B)
+        for e in lost:
+            if e < k:
+                wiped[:, e] = 0xA5
+        out = BO.decode_all(k, n, wiped.reshape(-1), par, B, N, surv)
+        assert BO.first_mismatch(out, data, L) is None

@@ -32,6 +32,7 @@
 #include <functional>
 #include <random>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "gf256.hpp"
@@ -154,6 +155,19 @@ std::vector<Var> variants() {
     h.heavy_first = true;
     v.push_back(h);
   }
+  // input-split tiles (rs_device.hpp rs_apply_desc_mix_ks): W waves x cap
+  auto ks = [&](auto WC, int cap) {
+    constexpr int W = decltype(WC)::value;
+    v.push_back({"input-split W=" + std::to_string(W) + " cap=" + std::to_string(cap), false, false,
+                 [cap](const DescArgs &a, const Bounds &, hipStream_t s) {
+                   return launch_desc_mix_ks<KM, W>(a, s, cap);
+                 },
+                 {}});
+  };
+  for (int cap : {0, 3, 4, 6, 8}) ks(std::integral_constant<int, 4>{}, cap);
+  for (int cap : {0, 6, 8, 12}) ks(std::integral_constant<int, 2>{}, cap);
+  if constexpr (KM == 32)
+    for (int cap : {0, 2, 3, 4}) ks(std::integral_constant<int, 8>{}, cap);
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
   if constexpr (KM == 16) {
