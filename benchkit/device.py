@@ -207,7 +207,8 @@ def download_leg(ctx, w, stream, a, reps=100):
                    "from simulated download arrivals, one storb_rs_decode_stripes_dev per batch",
            "ms_per_call": round(ms, 4), "calls": reps, "settle": settled,
            "host_us_per_call": round(host_us, 1),
-           "kernel": f"rs_apply_desc_mix<{min(k, 32)}>",
+           "kernel": (f"rs_apply_desc_mix_ks<{min(k, 32)}, 2>" if k == 16
+                      else f"rs_apply_desc_mix<{min(k, 32)}>"),
            "lost_data_shares_histogram": dict(sorted(hist.items())),
            "distinct_patterns": len({tuple(sorted(x)[:k]) for x in sets}),
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -217,7 +218,7 @@ def download_leg(ctx, w, stream, a, reps=100):
         # kernel time of the same mixed launch: a kernel-trace child run with
         # --erase-pattern download (its decode leg is this call), timed launches only
         kt = kernel_trace(a, w, a.settle_ms, "download",
-                          [leg_kernel_match(a, w, "encode"), "rs_apply_desc_mix<"])
+                          [leg_kernel_match(a, w, "encode"), "rs_apply_desc_mix"])
         if "legs" in kt:
             dk = kt["legs"]["decode"]
             # the child's own survivor sets (Workload, --erase-pattern download, rank 0)

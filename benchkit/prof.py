@@ -32,7 +32,7 @@ def leg_kernel_match(a, w, leg):
     """Substring of the rocprofv3 kernel name each leg launches (compiled
     kernels are named storb_bs_jit_k<k>_r<rows>_{ip,asm}, rs_jit.cpp)."""
     if leg == "decode" and w.sets is not None:
-        return "rs_apply_desc_mix<"
+        return "rs_apply_desc_mix"
     if leg in w.jit_legs:
         return f"storb_bs_jit_k{w.k}_r{jit_blocks(w.k, leg_rows(w, leg))[1]}_"
     if leg == "encode":
@@ -304,7 +304,8 @@ def kernel_names(kernel, w):
                            else jit_name(w, "encode") if "encode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")
     if "decode" in w.legs and w.sets is not None:
-        names["decode"] = (f"rs_apply_desc_mix<{min(w.k, 32)}> (per-stripe descriptors: one "
+        mix = "rs_apply_desc_mix_ks<16, 2>" if w.k == 16 else f"rs_apply_desc_mix<{min(w.k, 32)}>"
+        names["decode"] = (f"{mix} (per-stripe descriptors: one "
                            f"launch for the stripes that lost 1-4 data shares, one per larger "
                            f"count; descriptors copied in by copy_u32x4_kernel)")
     elif "decode" in w.legs:

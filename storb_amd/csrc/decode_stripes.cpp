@@ -151,6 +151,14 @@ int apply_desc(storb_rs_ctx *ctx, uint32_t k, size_t block, bool copy,
     if (!e && !copy) continue;
     (e <= kMixR ? mixg : by_r[e]).items.push_back(i);
   }
+  // The mixed launch's items heaviest first (most rebuilt rows): the
+  // workgroups with the longest folds start first, and the launch's tail is
+  // its lightest tiles (tools/mixbench.hip "heaviest items first": k = 32
+  // download mix 73.9-74.3 -> 74.7-75.7 % of 8 TB/s, profiles/r6i_mixbench32.txt,
+  // r6j_*; with k = 16's input-split tiles 77.2-77.4 -> 77.8-77.9 %).
+  std::stable_sort(mixg.items.begin(), mixg.items.end(), [&](uint32_t x, uint32_t y) {
+    return pats[x]->missing.size() > pats[y]->missing.size();
+  });
   std::vector<Group *> groups;
   if (!mixg.items.empty()) groups.push_back(&mixg);
   for (uint32_t e = kMixR + 1; e <= static_cast<uint32_t>(kSlotR); e++)

@@ -618,28 +618,86 @@ struct MixKs {
   static_assert(KM % W == 0, "W must divide the k bucket");
 };
 
+// One wave's part of an input-split tile: its KW inputs' loads are issued
+// FIRST, then the workgroup stages the item's tables in LDS (their global
+// loads overlap the share loads' latency instead of preceding it: the
+// record -> tables -> barrier -> share loads chain is what a short-lived
+// workgroup otherwise waits through twice), then the folds (inputs two at a
+// time, as perm_acc's PAIR), then the partial rows meet in LDS.
 template <int KM, int W, int R, bool GUARD>
-__device__ __forceinline__ void mix_ks_tile(const DescArgs &a, cu64 *rec, const PermTab *tabs,
+__device__ __forceinline__ void mix_ks_tile(const DescArgs &a, cu64 *rec, PermTab *lds_ptab,
                                             uint32_t cols, uint32_t c0, u32x4 *red) {
   using S = MixKs<KM, W>;
   constexpr int KW = S::KW;
-  constexpr int G = KW < Tune<KM, R>::G ? KW : Tune<KM, R>::G;
-  constexpr bool PAIR = mix_pair<KM, R>() && G % 2 == 0;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t j0 = w * KW;
   const uint32_t kw = a.k > j0 ? (a.k - j0 < KW ? a.k - j0 : KW) : 0u;
   const DescView v{rec, a.k, a.r};
-  const OffsetView<DescView> ov{v, j0};
-  u32x4 acc[R][1];
-  perm_acc<KW, R, 64, 1, false, G, PAIR, GUARD, false>(ov, tabs + j0 * R, kw, R, cols, c0, acc);
+  u32x4 buf[KW];
 #pragma unroll
-  for (int i = 0; i < R; i++) red[(w * R + i) * 64 + lane] = acc[i][0];
+  for (int jj = 0; jj < KW; jj++) {
+    if (jj >= static_cast<int>(kw)) {
+      buf[jj] = u32x4{0, 0, 0, 0};
+      continue;
+    }
+    const auto p = v.in(static_cast<int>(j0) + jj);
+    buf[jj] = (!GUARD || c0 < cols) ? ld_stream(p + c0) : u32x4{0, 0, 0, 0};
+  }
+  {
+    typedef const PermTab __attribute__((address_space(4))) cPermTab;
+    typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
+    cPermTab *gt = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
+    const uint32_t n16 = a.k * R * (sizeof(PermTab) / 16);
+    for (uint32_t t = threadIdx.x; t < n16; t += S::T)
+      reinterpret_cast<u32x4 *>(lds_ptab)[t] = ((gcu32x4 *)(gt))[t];
+    // LDS writes done, then the workgroup barrier; no vmcnt wait for the
+    // share loads beyond what the table writes needed (__syncthreads' fences
+    // would wait for every outstanding load)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  const PermTab *tabs = lds_ptab + j0 * R;
+  u32x4 acc[R];
+#pragma unroll
+  for (int i = 0; i < R; i++) acc[i] = u32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int jj = 0; jj < KW; jj += 2) {
+    if (jj >= static_cast<int>(kw)) continue;
+    const bool two = jj + 1 < static_cast<int>(kw);
+    uint32_t s0[2][4], s1[2][4], s2[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t d = (h == 0 || two) ? buf[jj + h][q] : 0u;
+        s0[h][q] = d & 0x07070707u;
+        s1[h][q] = (d >> 3) & 0x07070707u;
+        s2[h][q] = (d >> 6) & 0x03030303u;
+      }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+      const PermTab ta = tabs[jj * R + i];
+      const PermTab tb = two ? tabs[(jj + 1) * R + i] : PermTab{};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t x = acc[i][q];
+        x = xor3(x, __builtin_amdgcn_perm(ta.t0hi, ta.t0lo, s0[0][q]),
+                 __builtin_amdgcn_perm(ta.t1hi, ta.t1lo, s1[0][q]));
+        x = xor3(x, __builtin_amdgcn_perm(0u, ta.t2, s2[0][q]),
+                 __builtin_amdgcn_perm(tb.t0hi, tb.t0lo, s0[1][q]));
+        x = xor3(x, __builtin_amdgcn_perm(tb.t1hi, tb.t1lo, s1[1][q]),
+                 __builtin_amdgcn_perm(0u, tb.t2, s2[1][q]));
+        acc[i][q] = x;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; i++) red[(w * R + i) * 64 + lane] = acc[i];
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
   for (int i = 0; i < R; i++) {
     if (i % W != static_cast<int>(w)) continue;  // wave-uniform
-    u32x4 x = acc[i][0];
+    u32x4 x = acc[i];
 #pragma unroll
     for (int q = 0; q < W; q++)
       if (q != static_cast<int>(w)) x ^= red[(q * R + i) * 64 + lane];
@@ -657,14 +715,6 @@ __global__ __launch_bounds__((MixKs<KM, W>::T)) void rs_apply_desc_mix_ks(const 
   const uint32_t base = (blockIdx.x - item * tps) * 64;
   cu64 *rec = (cu64 *)(a.desc) + static_cast<uint64_t>(item) * a.rec_qwords;
   const uint32_t r = static_cast<uint32_t>(rec[0] >> 32);
-  const uint32_t rb = r <= 1 ? 1 : r;  // rows of the item's tables ([input][rb])
-  typedef const PermTab __attribute__((address_space(4))) cPermTab;
-  typedef const u32x4 __attribute__((address_space(1))) gcu32x4;
-  cPermTab *gt = (cPermTab *)(a.ptab) + (rec[0] & 0xFFFFFFFFu);
-  const uint32_t n16 = a.k * rb * (sizeof(PermTab) / 16);
-  for (uint32_t t = threadIdx.x; t < n16; t += MixKs<KM, W>::T)
-    reinterpret_cast<u32x4 *>(lds_ptab)[t] = ((gcu32x4 *)(gt))[t];
-  __syncthreads();
   const uint32_t c0 = base + (threadIdx.x & 63);
   const bool full = base + 64 <= cols;
 #define STORB_MIXKS_CASE(R)                                                          \
@@ -795,8 +845,20 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
 // k <= 4 with one-wave workgroups (mix_threads): 16 per CU.
 constexpr int mix_occ(int KM) { return KM <= 4 ? 16 : KM == 32 ? 3 : 0; }
 
+// k = 16 (config 5's download mix) runs the input-split tiles, two waves per
+// 1 KiB tile (rs_apply_desc_mix_ks<16, 2>), uncapped: tools/mixbench.hip on
+// config 5's download shape, records heaviest first as apply_desc orders
+// them, 76.0-76.7 -> 77.8-77.9 % of 8 TB/s (profiles/r6i_mixbench16.txt,
+// r6j_mixbench16.txt); four waves per tile 70-71 %. At k = 32 neither two,
+// four nor eight waves gained (72.7-74.4 against 74.7 %), so it keeps the
+// one-wave-per-256-lane shape. Fused assembly (copy) keeps rs_apply_desc_mix.
+template <int KM>
+constexpr int mix_ks_waves() { return KM == 16 ? 2 : 0; }
+
 template <int KM>
 hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
+  if constexpr (mix_ks_waves<KM>() > 0)
+    if (!a.copy && a.tpw == 1) return launch_desc_mix_ks<KM, mix_ks_waves<KM>()>(a, s, a.cap);
   constexpr uint64_t TILE = mix_threads<KM>();
   const uint64_t tps = ((a.block >> 4) + TILE - 1) / TILE;
   if (a.tpw != 1) return hipErrorInvalidConfiguration;  // one tile per workgroup

@@ -206,18 +206,25 @@ def download_survivors(k: int, m: int, rng: np.random.Generator, fail=(),
 
 def reconstruct_object(chunks: Sequence[ChunkValue], fetched: Sequence[Dict[int, bytes]],
                        ctx: Optional[_lib.Context] = None,
-                       contexts: Optional[Sequence[_lib.Context]] = None) -> np.ndarray:
+                       contexts: Optional[Sequence[_lib.Context]] = None,
+                       out: Optional[np.ndarray] = None) -> np.ndarray:
     """The download side: fetched[c] maps piece_idx -> piece bytes of chunk c
     (any subset); each chunk rebuilds from its first k pieces by index
     (reconstruct_chunk); PieceError if a chunk has fewer than k. One batched
     GPU call per run of chunks of one geometry. Returns the object's bytes
-    as a uint8 array (no extra copy into a bytes object)."""
+    as a uint8 array (no extra copy into a bytes object), written into `out`
+    when given (a download buffer the caller reuses: a fresh one is first
+    touched page by page while the decoded chunks land in it)."""
     ctxs = list(contexts) if contexts else [ctx or _lib.thread_context()]
     for ci, (cv, got) in enumerate(zip(chunks, fetched)):
         if len(got) < cv.k:
             raise PieceError(ci, cv.k, len(got))
     total = sum(cv.original_chunk_size for cv in chunks)
-    out = np.empty(total, np.uint8)
+    if out is None:
+        out = np.empty(total, np.uint8)
+    elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < total:
+        raise ValueError("out: a contiguous uint8 buffer of the object's size")
+    out = out[:total]
     geo = [(cv.k, cv.m, cv.chunk_size, cv.padlen, cv.original_chunk_size) for cv in chunks]
     off = 0
     i = 0

@@ -259,6 +259,14 @@ def _run(a, miners, inspect=None):
     t_decode = time.perf_counter() - t2
     t_download = time.perf_counter() - t1
     ok = bool(np.array_equal(out, obj))
+    # the same reconstruct into a download buffer the validator reuses (the
+    # fresh one above is first-touched page by page as the chunks land in it;
+    # the bench's pcie_inclusive decode figures write pre-touched buffers)
+    t3 = time.perf_counter()
+    again = objects.reconstruct_object(enc.chunks, [gathered[ci] for ci in range(len(metas))],
+                                       contexts=ctxs, out=out)
+    t_decode_reused = time.perf_counter() - t3
+    ok = ok and bool(np.array_equal(again, obj))
     nshards = sum(m["m"] for m in metas)
     res = {
         "config": "BASELINE 5 loopback (validator + miners on 127.0.0.1)",
@@ -278,9 +286,11 @@ def _run(a, miners, inspect=None):
         # harness's Python socket legs, which bound the end-to-end figure
         "gpu_legs": {"encode_with_piece_ids_GiBps": round(a.size / GIB / t_encode, 3),
                      "batched_reconstruct_GiBps": round(a.size / GIB / t_decode, 3),
+                     "batched_reconstruct_reused_out_GiBps": round(a.size / GIB / t_decode_reused, 3),
                      "what": "objects.encode_object (storb_rs_encode_chunks_hashed) and "
                              "objects.reconstruct_object (storb_rs_decode_chunks), host "
-                             "buffers in and out, PCIe included"},
+                             "buffers in and out, PCIe included; reused_out = the same into "
+                             "an already-touched object buffer"},
         "harness_legs": {"store_framing_upload_s": round(t_upload - t_encode, 4),
                          "python_fetch_s": round(t_fetch, 4),
                          "what": "Python sockets / HTTP of this harness (wire.py), not the "

@@ -156,18 +156,21 @@ std::vector<Var> variants() {
     v.push_back(h);
   }
   // input-split tiles (rs_device.hpp rs_apply_desc_mix_ks): W waves x cap
-  auto ks = [&](auto WC, int cap) {
+  auto ks = [&](auto WC, int cap, bool heavy) {
     constexpr int W = decltype(WC)::value;
-    v.push_back({"input-split W=" + std::to_string(W) + " cap=" + std::to_string(cap), false, false,
-                 [cap](const DescArgs &a, const Bounds &, hipStream_t s) {
-                   return launch_desc_mix_ks<KM, W>(a, s, cap);
-                 },
-                 {}});
+    Var x{"input-split W=" + std::to_string(W) + " cap=" + std::to_string(cap) +
+              (heavy ? " heavy first" : ""), false, false,
+          [cap](const DescArgs &a, const Bounds &, hipStream_t s) {
+            return launch_desc_mix_ks<KM, W>(a, s, cap);
+          },
+          {}};
+    x.heavy_first = heavy;
+    v.push_back(x);
   };
-  for (int cap : {0, 3, 4, 6, 8}) ks(std::integral_constant<int, 4>{}, cap);
-  for (int cap : {0, 6, 8, 12}) ks(std::integral_constant<int, 2>{}, cap);
-  if constexpr (KM == 32)
-    for (int cap : {0, 2, 3, 4}) ks(std::integral_constant<int, 8>{}, cap);
+  for (bool heavy : {false, true}) {
+    for (int cap : {0, 8, 10, 12, 16}) ks(std::integral_constant<int, 2>{}, cap, heavy);
+    for (int cap : {0, 8}) ks(std::integral_constant<int, 4>{}, cap, heavy);
+  }
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
   if constexpr (KM == 16) {
