@@ -99,7 +99,7 @@ static int encode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n,
   // Page-locked caller chunks without piece ids: the kernel reads them (and
   // writes parity) over PCIe directly (zero-copy). Kernel-driven PCIe
   // traffic overlaps both directions, where the SDMA copies of H2D and D2H
-  // share one ceiling (57 GB/s total, tools/pcie_probe.py): 47 vs 35 GiB/s
+  // share one ceiling (57 GB/s total, round 1's PCIe probe; the bench line measures it now): 47 vs 35 GiB/s
   // measured. From pageable chunks the SDMA pipeline stays ahead (34 vs
   // 20 GiB/s: the host's packing competes with the kernel's reads of the
   // same staging), and the hashed path keeps the shares on the device.

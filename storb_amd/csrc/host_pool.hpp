@@ -130,7 +130,7 @@ class HostPool {
   }
 
   // How many threads a copy of `total` bytes into page-locked memory takes.
-  // Measured (tools/poolbench.cpp, profiles/r3_poolbench.txt, GPU-box host):
+  // Measured (the removed poolbench, profiles/r3_poolbench.txt, GPU-box host):
   // one thread copies 256 KiB in 1.7 us and 1 MiB in 21 us; two threads 1 MiB
   // in 5.2 us, while 4 or 8 (waking, claiming parts) took 13-20 us; from
   // 4 MiB on 8 threads win (28-35 us against 44 for two, 84 for one). Inside

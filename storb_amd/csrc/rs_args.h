@@ -129,9 +129,9 @@ constexpr unsigned bs_cols_per_tile(int threads) { return 2u * static_cast<unsig
 
 // Launch shape per (k, rows), from the sweep of workgroup size x tile
 // rotation x resident-workgroup cap: over the kernels alone
-// (tools/bstune.hip, profiles/r2_bstune_shape*.txt; tools/wide_probe.hip for
+// (tools/bstune.hip, profiles/r2_bstune_shape*.txt; profiles/r2_wide_probe_2.txt for
 // the access shape with no GF work) and on the product's own decode path
-// (tools/shape_ab.sh, profiles/r2_shape_ab/: bench --config 5/6 --erase E).
+// (a removed A/B script, profiles/r2_shape_ab/: bench --config 5/6 --erase E).
 // The wide shapes stream best with few bytes in flight per CU and no
 // workgroup waiting long on its slowest wave: one-wave workgroups, 6 per CU,
 // for 6+ rows at k <= 16 (RS(16,8) encode 0.267 -> 0.257 ms, 8-lost decode
@@ -173,7 +173,7 @@ constexpr int bs_group(int K, int R) {
 // half per wave), one input per wave per load group. Used (bs_split)
 //  * for 17-32 rows -- Storb's k = 64 encode and decodes losing more than 16
 //    shares -- which one wave cannot hold: 4 workgroups per CU (2 waves per
-//    SIMD at ~197 VGPRs). tools/k64split.hip, k = 64 encode of 8 x 128 MiB
+//    SIMD at ~197 VGPRs). the removed k64split probe, k = 64 encode of 8 x 128 MiB
 //    chunks: 494.6 us as two 16-row launches -> 348.6 us; 3 per CU 556 us
 //    (6 waves per CU), uncapped 391, 2 inputs per wave per group 376
 //    (profiles/r2_k64/k64split.txt);
@@ -189,6 +189,33 @@ constexpr int kSplitThreads = 128;           // two waves, one row half each
 constexpr unsigned kSplitColsPerTile = 128;  // 64 lanes x 2 16-B columns
 // Static LDS of one workgroup: [group parity][owner wave][G/2 inputs][2 halves][64 lanes] x 16 B.
 constexpr unsigned split_lds_bytes(int G) { return 2u * 2u * static_cast<unsigned>(G / 2) * 2u * 64u * 16u; }
+
+// Input-split form (rs_bitslice_core.h bs_ksplit_body): C column groups of W
+// waves per workgroup, W waves on the same 2 KiB of every share, each folding
+// K / W inputs (G per load group); cap resident per CU. c = 0: not used (one
+// wave per tile, bs_shape). Measured (tools/bstune.hip BSTUNE_KSPLIT, every
+// variant bit-exact against the one-wave kernel; profiles/r6e_bstune_ksplit.txt
+// for the encoders, r6n/bstune_dec.txt for the in-place decodes): RS(16,8)
+// encode 79.3-80.1 -> 81.0-81.7 % of 8 TB/s (C 1 W 4), k = 16 decode of 8
+// lost 80.7 -> 82.4 % (C 1 W 4), of 4 lost 77.5 -> 80.1 % (C 2 W 2), RS(32,16)
+// encode 74.0 -> 75.4 % and k = 32 decode of 16 lost 74.1 -> 76.5 % (C 2 W 2);
+// k = 16 decode of 2 lost 82.1 -> 79.5 % and k = 32 of 2 lost equal, so few
+// rows keep one wave per tile.
+struct KsShape {
+  int c, w, g, cap;
+};
+constexpr int ks_group(int KW) { return KW % 4 == 0 ? 4 : KW % 2 == 0 ? 2 : 1; }
+constexpr KsShape ks_shape(int K, int R) {
+  return (K <= 16 && R == 8 && K % 4 == 0)   ? KsShape{1, 4, ks_group(K / 4), 4}
+         : (K <= 16 && R == 4 && K % 2 == 0) ? KsShape{2, 2, ks_group(K / 2), 3}
+         : (K > 16 && R == 16 && K % 2 == 0) ? KsShape{2, 2, ks_group(K / 2), 2}
+                                             : KsShape{0, 0, 0, 0};
+}
+// Static LDS of an input-split workgroup: per column group
+// [owner wave][partner (W-1)][row of owner (R/W)][2 halves][64 lanes] x 16 B.
+constexpr unsigned ksplit_lds_bytes(int C, int W, int R) {
+  return W > 1 ? static_cast<unsigned>(C * W * (W - 1) * (R / W) * 2 * 64 * 16) : 16u;
+}
 
 }  // namespace bs
 

@@ -122,8 +122,9 @@ struct BsTune {
 // one-wave tiles at 80.1 / 77.4 %.
 template <int K, int N>
 struct KsTune {
-  static constexpr bool ON = (K == 16 && N == 24) || (K == 32 && N == 48);
-  static constexpr int C = K == 16 ? 1 : 2, W = K == 16 ? 4 : 2, G = 4, CAP = K == 16 ? 4 : 2;
+  static constexpr KsShape S = ks_shape(K, N - K);  // rs_args.h
+  static constexpr bool ON = S.c > 0;
+  static constexpr int C = ON ? S.c : 1, W = ON ? S.w : 1, G = ON ? S.g : 1, CAP = S.cap;
   static constexpr uint64_t CPT = 128u * C;
 };
 

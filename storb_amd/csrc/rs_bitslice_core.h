@@ -98,7 +98,8 @@ __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // Loads: non-temporal (shares are read once) unless STORB_BS_LOAD_NT=0
-// (tools/k64pair.hip: whether cached loads let a second reader hit).
+// (the removed k64pair probe, profiles/r2_k64/k64pair.txt: whether cached loads let a
+// second reader hit).
 #ifndef STORB_BS_LOAD_NT
 #define STORB_BS_LOAD_NT 1
 #endif
@@ -256,7 +257,7 @@ __device__ __forceinline__ void bs_tile(const ApplyArgs &a, uint32_t stripe, uin
 // T lanes per workgroup, each wave covering 2 KiB of every share. SWZ = 1
 // rotates the tile order of stripe s by s * (tiles / 8 + 1), so the
 // workgroups of neighbouring stripes that run at the same moment stream
-// from different offsets of their shares (tools/wide_probe.hip).
+// from different offsets of their shares (profiles/r2_wide_probe_2.txt).
 // ------------------------------------------------------------ row-split form
 // Matrices of more than 16 rows (Storb's k = 64 geometry: 32 parity rows,
 // and decodes losing more than 16 shares of it). One lane cannot hold 32 x 8
@@ -404,9 +405,7 @@ __device__ __forceinline__ void bs_split_body(const ApplyArgs &a) {
 // CU, 16 shares x 2 KiB each in flight, and stream below the 4 KiB-per-
 // workgroup probe shape).
 // LDS per column group: [owner wave d][partner q (W-1)][row of d (R/W)][2 halves][64 lanes] x 16 B.
-constexpr unsigned ksplit_lds_bytes(int C, int W, int R) {
-  return W > 1 ? static_cast<unsigned>(C * W * (W - 1) * (R / W) * 2 * 64 * 16) : 16u;
-}
+// (ksplit_lds_bytes: rs_args.h)
 template <int C, int W, int R>
 struct KsplitLds {
   v4 v[ksplit_lds_bytes(C, W, R) / 16];

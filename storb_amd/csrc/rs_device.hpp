@@ -44,7 +44,7 @@ static constexpr int kThreads = 256;
 // k*RM nibble tables in LDS at block start and read them as broadcast
 // ds_reads instead of s_loads.
 // Resident workgroups per CU (rs_kernels.hpp wg_cap; 0 = uncapped), from
-// the product-level sweep tools/occ_sweep.py (profiles/r1_occupancy.txt):
+// the product-level sweep (a removed script) (profiles/r1_occupancy.txt):
 // RS(4,2) encode / decode 6.40 -> 6.65 TB/s at 4, its one-row repair +5-7 %,
 // RS(16,2) decode (config 5) +13 % at 2, RS(16,1) repair +9 % at 4; RS(8,4)
 // encode, config 3's <8,3> decode and the 8-row k = 16 decode +1-4 % at 4

@@ -398,7 +398,7 @@ Jit &jit() {
 // encoders); the resident-workgroup cap is an LDS reservation
 // (rs_kernels.hpp cap_lds, see dynamic_lds()).
 // (Round 2 swept it on the real decode path with a run-time override,
-// tools/shape_ab.sh, profiles/r2_shape_ab/; the override is gone.)
+// a removed A/B script, profiles/r2_shape_ab/; the override is gone.)
 bs::BsShape shape(uint32_t k, uint32_t r) {
   return bs::bs_shape(static_cast<int>(k), static_cast<int>(r));
 }
@@ -411,13 +411,40 @@ bs::BsShape split_or_shape(uint32_t k, uint32_t r) {
   return bs::BsShape{bs::kSplitThreads, 0, bs::bs_split_cap(static_cast<int>(r))};
 }
 
+// The input-split form (rs_args.h ks_shape) where it measured faster: k <=
+// 16 with 4 or 8 rows, k > 16 with 16 rows (c = 0: not used).
+// (Not with fused assembly at k > 16: the k = 32 16-row kernel that also
+// stores its inputs spilled 171 VGPRs at -O1 in the input-split form; the
+// in-place one took 249, none spilled.)
+bs::KsShape ks_of(uint32_t k, uint32_t r, uint64_t copy_mask) {
+  if (split_rows(k, r) || (copy_mask && k > 16)) return bs::KsShape{0, 0, 0, 0};
+  return bs::ks_shape(static_cast<int>(k), static_cast<int>(r));
+}
+
+// Threads, 16-B columns per tile and LDS reservation of a JIT launch.
+struct LaunchShape {
+  int threads;
+  uint64_t cpt;
+  size_t lds;
+};
+LaunchShape launch_shape(uint32_t k, uint32_t r, uint64_t copy_mask) {
+  const bs::KsShape ks = ks_of(k, r, copy_mask);
+  if (ks.c)
+    return {64 * ks.c * ks.w, 128u * static_cast<uint64_t>(ks.c),
+            cap_lds(ks.cap, bs::ksplit_lds_bytes(ks.c, ks.w, static_cast<int>(r)))};
+  const bool split = split_rows(k, r);
+  const bs::BsShape sh = split_or_shape(k, r);
+  return {sh.threads, split ? bs::kSplitColsPerTile : bs::bs_cols_per_tile(sh.threads),
+          cap_lds(sh.cap, split ? bs::split_lds_bytes(bs::kSplitGroup) : 0)};
+}
+
 // The cap's LDS reservation is requested at launch (dynamic LDS) when it is
 // at most 64 KiB (caps >= 3; above that a kernel must opt in) and baked into
 // the source as a static array otherwise. Static LDS that limits occupancy
 // to 2 waves per SIMD told the register allocator it could use all 256
 // VGPRs, and it did: the k = 64 row-split encode took 256 VGPRs with 7
 // spilled (0.535 ms in bench --config 7) against 197 and none with the same
-// reservation made at launch (0.349 ms in tools/k64split.hip); likewise the
+// reservation made at launch (0.349 ms in the removed k64split probe, profiles/r2_k64/k64split.txt); likewise the
 // 16-row blocks 229 vs 196 (profiles/r2_k64/split_dynlds_ab.txt).
 size_t dynamic_lds(size_t lds) { return lds <= (64u << 10) ? lds : 0; }
 
@@ -453,7 +480,8 @@ bool split_rows(uint32_t k, uint32_t rows) {
 // The kernel source for a (rows x k) matrix: bit b' of row[p][j][b] is bit b
 // of coef[p][j] * 2^b' (the GF(2) matrix of multiplication by coef[p][j]).
 std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask,
-                   int group, const bs::BsShape &sh, size_t lds, bool split) {
+                   int group, const bs::BsShape &sh, size_t lds, bool split,
+                   const bs::KsShape &ks) {
   const GF256 &g = gf();
   std::string s;
   s.reserve(64 + static_cast<size_t>(rows) * k * 40);
@@ -486,7 +514,8 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
   }
   // 2 waves per SIMD (<= 256 registers): without the hint, 64- and 128-lane
   // workgroups let the allocator take 257 at k = 32 (1 wave per SIMD)
-  s += "extern \"C\" __global__ __launch_bounds__(" + std::to_string(sh.threads) +
+  const int threads = ks.c ? 64 * ks.c * ks.w : sh.threads;
+  s += "extern \"C\" __global__ __launch_bounds__(" + std::to_string(threads) +
        ") __attribute__((amdgpu_waves_per_eu(2))) void " + kernel_name(k, rows, copy_mask) +
        "(const storb_rs::ApplyArgs a) {\n";
   if (test_call()) s += "  storb_jit_test_callee(a);\n";
@@ -495,7 +524,10 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
     s += "  __shared__ unsigned occ_pad[" + std::to_string(lds / 4) + "];\n";
     s += "  asm volatile(\"\" :: \"s\"(occ_pad));  // keeps the unused array allocated\n";
   }
-  if (split)
+  if (ks.c)
+    s += "  storb_rs::bs::bs_ksplit_body<JitMat, " + std::to_string(ks.c) + ", " +
+         std::to_string(ks.w) + ", " + std::to_string(ks.g) + ", 1>(a);\n}\n";
+  else if (split)
     s += "  storb_rs::bs::bs_split_body<JitMat, " + std::to_string(group) + ", " +
          std::to_string(sh.swz) + ">(a);\n}\n";
   else
@@ -509,7 +541,7 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
 bool enabled() { return mode() != Mode::Off; }
 
 // Worth a compiled kernel where it beats the table kernel -- measured A/B on
-// the GPU with the launch shapes of rs_args.h bs_shape (tools/compare_jit.sh,
+// the GPU with the launch shapes of rs_args.h bs_shape (a removed A/B script,
 // STORB_RS_JIT=0 vs =always, profiles/r2_jit_policy_ab2/; bench decode leg
 // ms, table / compiled): k = 16: r = 2 0.195 / 0.189, r = 3 0.219 / 0.204,
 // r = 4 0.235 / 0.218, r = 8 0.397 / 0.256; k = 32: r = 2 0.230 / 0.187,
@@ -537,17 +569,20 @@ static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *c
   const bool split = split_rows(k, r);
   const int group = split ? bs::kSplitGroup : bs::bs_group(static_cast<int>(k), static_cast<int>(r));
   const bs::BsShape sh = split_or_shape(k, r);
-  const size_t lds = cap_lds(sh.cap, split ? bs::split_lds_bytes(bs::kSplitGroup) : 0);
+  const bs::KsShape ks = ks_of(k, r, copy_mask);
+  const size_t lds = launch_shape(k, r, copy_mask).lds;
   std::string key(32 + static_cast<size_t>(r) * k, '\0');
   const uint64_t hdr[4] = {(static_cast<uint64_t>(k) << 32) | r, copy_mask,
                            (static_cast<uint64_t>(group) << 32) | lds,
                            (static_cast<uint64_t>(sh.threads) << 32) | static_cast<uint32_t>(sh.swz) |
-                               (split ? 1ull << 16 : 0)};
+                               (split ? 1ull << 16 : 0) |
+                               (static_cast<uint64_t>(ks.c * 16 + ks.w) << 20) |
+                               (static_cast<uint64_t>(ks.g) << 26)};
   std::memcpy(&key[0], hdr, sizeof(hdr));
   std::memcpy(&key[32], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
   auto e = J.get(key, kernel_name(k, r, copy_mask), opt_level(k),
-                 [&] { return source(k, r, coef, copy_mask, group, sh, lds, split); }, force);
+                 [&] { return source(k, r, coef, copy_mask, group, sh, lds, split, ks); }, force);
   if (e && wait) J.wait_for(*e);
   return e;
 }
@@ -613,10 +648,8 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
   hipError_t r = hipSuccess;
   for (uint32_t b = 0; b < nb && r == hipSuccess; b++) {
     const uint32_t r0 = row_start(a.k, a.r, b), rr = row_start(a.k, a.r, b + 1) - r0;
-    const bs::BsShape sh = split_or_shape(a.k, rr);
-    const uint64_t cpt =
-        split_rows(a.k, rr) ? bs::kSplitColsPerTile : bs::bs_cols_per_tile(sh.threads);
-    const uint64_t blocks = ((cols + cpt - 1) / cpt) * a.nstripes;
+    const LaunchShape ls = launch_shape(a.k, rr, b == 0 ? copy_mask : 0);
+    const uint64_t blocks = ((cols + ls.cpt - 1) / ls.cpt) * a.nstripes;
     if (blocks == 0 || blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     ApplyArgs arg = a;
     arg.r = rr;
@@ -629,10 +662,9 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
       arg.out_stride[i] = out_stride[r0 + i];
     }
     void *params[] = {&arg};
-    const size_t lds = cap_lds(sh.cap, split_rows(a.k, rr) ? bs::split_lds_bytes(bs::kSplitGroup) : 0);
     r = hipModuleLaunchKernel(fs[b], static_cast<unsigned>(blocks), 1, 1,
-                              static_cast<unsigned>(sh.threads), 1, 1,
-                              static_cast<unsigned>(dynamic_lds(lds)), s, params, nullptr);
+                              static_cast<unsigned>(ls.threads), 1, 1,
+                              static_cast<unsigned>(dynamic_lds(ls.lds)), s, params, nullptr);
     if (r == hipSuccess) r = J.used(*es[b], device, s);
     if (r == hipSuccess) J.launches++;
   }

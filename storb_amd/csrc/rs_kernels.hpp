@@ -32,7 +32,7 @@ enum class Variant { Perm = 1, Lds = 2 };
 // "occ", profiles/r1_occupancy.txt). The cap is imposed by reserving LDS:
 // a workgroup asks for 160 KiB / cap, so cap fit on a CU and cap + 1 do not.
 // (The caps were swept in round 1 with a run-time override,
-// tools/occ_sweep.py, profiles/r1_occupancy.txt; the override is gone.)
+// the removed occ_sweep script, profiles/r1_occupancy.txt; the override is gone.)
 constexpr size_t kLdsPerCu = 160u << 10;
 inline int wg_cap(int tuned) { return tuned; }
 // Dynamic LDS to request so at most `cap` workgroups with `static_lds`

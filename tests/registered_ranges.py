@@ -7,7 +7,7 @@ Registering caller memory creates a device mapping of it; unregistering
 tears that mapping down and frees its device addresses. This round saw two
 illegal-address faults in torch host->device copies later in a pytest
 process that had run these checks early (cause not found; no
-stale mapping visible to HIP, tools/register_probe.py). Running the checks in
+stale mapping visible to HIP, the removed register_probe). Running the checks in
 their own process keeps whatever registration does to the process's GPU
 address space out of the rest of the suite. Each case is oracle-exact.
 

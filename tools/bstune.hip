@@ -211,19 +211,25 @@ void run(const char *name, uint32_t nstripes, uint64_t B, int rounds, bool dec =
       add<K, N, 4, 128, 1>(vs, {3});
     }
   } else if (std::getenv("BSTUNE_KSPLIT")) {  // input-split workgroups x cap
+    if (dec) {  // the JIT decode kernels' shape first (rs_args.h bs_shape): the reference
+      constexpr bs::BsShape S = bs::bs_shape(K, R);
+      add<K, N, G, S.threads, S.swz>(vs, {S.cap});
+    }
     if constexpr (R == 8) {
-      add_ks<K, N, 2, 2, 8, 1>(vs, {1, 2, 3});
-      add_ks<K, N, 2, 2, 4, 1>(vs, {1, 2, 3});
-      add_ks<K, N, 2, 2, 8, 0>(vs, {2});
-      add_ks<K, N, 1, 4, 4, 1>(vs, {2, 4});
-      add_ks<K, N, 1, 2, 8, 1>(vs, {4});
+      add_ks<K, N, 1, 4, 4, 1>(vs, {4});
+      add_ks<K, N, 2, 2, 8, 1>(vs, {2, 3});
+      add_ks<K, N, 2, 2, 4, 1>(vs, {2, 3});
     }
     if constexpr (R == 16) {
-      add<K, N, G, 128, 0>(vs, {2, 3, 4});
-      add_ks<K, N, 2, 2, 2, 1>(vs, {1, 2});
-      add_ks<K, N, 2, 2, 4, 1>(vs, {1, 2});
-      add_ks<K, N, 2, 2, 8, 1>(vs, {1, 2});
-      add_ks<K, N, 1, 2, 4, 1>(vs, {2, 4});
+      add_ks<K, N, 2, 2, 4, 1>(vs, {2});
+      add_ks<K, N, 2, 2, 2, 1>(vs, {2});
+    }
+    if constexpr (R == 2 || R == 4) {
+      add_ks<K, N, 1, 2, 4, 1>(vs, {3, 4, 6, 8});
+      add_ks<K, N, 2, 2, 4, 1>(vs, {2, 3, 4});
+      if constexpr (K / 2 % 8 == 0) add_ks<K, N, 2, 2, 8, 1>(vs, {2, 3, 4});
+      if constexpr (K % 4 == 0 && R == 4) add_ks<K, N, 1, 4, 4, 1>(vs, {2, 3, 4});
+      if constexpr (K % 4 == 0 && R == 4) add_ks<K, N, 2, 4, 4, 1>(vs, {1, 2});
     }
   } else if (std::getenv("BSTUNE_LOWCAP")) {  // fewer bytes in flight per CU
     add<K, N, G, 64, 1>(vs, {2, 3, 4, 6});
@@ -329,6 +335,14 @@ int main(int argc, char **argv) {
     run<32, 34>("decode k=32, 2 lost (in place)", 32, 1 << 20, rounds, true);
     run<32, 36>("decode k=32, 4 lost (in place)", 32, 1 << 20, rounds, true);
     run<32, 40>("decode k=32, 8 lost (in place)", 32, 1 << 20, rounds, true);
+    return 0;
+  }
+  if (which == 5) {  // decodes for the input-split JIT shapes (BSTUNE_KSPLIT)
+    run<16, 18>("decode k=16, 2 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    run<16, 20>("decode k=16, 4 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    run<16, 24>("decode k=16, 8 lost, 128 x 8 MiB (in place)", 128, 512 << 10, rounds, true);
+    run<32, 34>("decode k=32, 2 lost, 32 x 32 MiB (in place)", 32, 1 << 20, rounds, true);
+    run<32, 48>("decode k=32, 16 lost, 32 x 32 MiB (in place)", 32, 1 << 20, rounds, true);
     return 0;
   }
   if (which == 3) {
