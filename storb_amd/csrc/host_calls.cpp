@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "rs_jit.hpp"
 #include "seq.hpp"
 
 using namespace storb_rs;
@@ -175,9 +176,16 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
   const uint32_t bs_cpt = enc_n ? bitslice_stream_cols_per_tile(k, enc_n) : 0;
   // (The table kernel streams up to k = 32, but measured at k = 32 -- (32, 48)
   // 32 MiB decode 2.32 ms against 0.94 ms on the sliced path, whose
-  // compiled bit-sliced kernels read wider -- it stays for k <= 16.)
-  if (!bs_cpt && (k > 16 || rows > 8)) return kNotStreamed;
-  const uint32_t cpt = bs_cpt ? bs_cpt : static_cast<uint32_t>(kThreadsTable);
+  // compiled bit-sliced kernels read wider -- it stays for k <= 16.) Above
+  // k = 16, with STORB_RS_JIT_STREAM=1, the matrix's compiled kernel in its
+  // streamed form (rs_jit.cpp try_launch_stream) once it is compiled; off by
+  // default, measured slower than the sliced path (rs_jit.cpp stream_enabled).
+  const bool jit_st = !bs_cpt && k > 16 && jit::stream_form(k, rows) &&
+                      jit::wanted(k, rows, static_cast<uint64_t>(k + rows) * S);
+  if (!bs_cpt && !jit_st && (k > 16 || rows > 8)) return kNotStreamed;
+  const uint32_t cpt = bs_cpt ? bs_cpt
+                              : jit_st ? jit::stream_cols_per_tile(k, rows)
+                                       : static_cast<uint32_t>(kThreadsTable);
   const uint32_t cols = static_cast<uint32_t>(S / 16);
   // 64 KiB of every share per slice, at most kMaxStreamSlices slices
   uint32_t slice_cols = 4096;
@@ -196,7 +204,7 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
   }
   Tables *t = nullptr;
   int rc;
-  if (!bs_cpt && (rc = get_tables(ctx, k, rows, coef, s, &t))) return rc;
+  if (!bs_cpt && !jit_st && (rc = get_tables(ctx, k, rows, coef, s, &t))) return rc;
   ApplyArgs a{};
   a.k = k;
   a.r = rows;
@@ -229,10 +237,16 @@ int streamed(storb_rs_ctx *ctx, uint32_t k, uint32_t rows, const uint8_t *coef,
     tiles[i] = (len + cpt - 1) / cpt;
     st.target[i] = ctx->sbase[i] + tiles[i];
   }
-  const hipError_t le = bs_cpt ? launch_encode_bitslice_stream(a, enc_n, st, s)
-                              : launch_apply_stream(a, st, s);
-  if (le == hipErrorInvalidValue) return kNotStreamed;  // nothing was queued
-  HIP_TRY(ctx, le);
+  if (jit_st) {
+    bool launched = false;
+    HIP_TRY(ctx, jit::try_launch_stream(ctx->device, a, coef, st, s, &launched));
+    if (!launched) return kNotStreamed;  // not compiled yet: nothing was queued
+  } else {
+    const hipError_t le = bs_cpt ? launch_encode_bitslice_stream(a, enc_n, st, s)
+                                : launch_apply_stream(a, st, s);
+    if (le == hipErrorInvalidValue) return kNotStreamed;  // nothing was queued
+    HIP_TRY(ctx, le);
+  }
   if (t && (rc = tables_used(ctx, t, s))) return rc;
   uint32_t *ready_h = reinterpret_cast<uint32_t *>(ctx->sword_pin.p);
   const uint32_t *done_h = ready_h + kMaxStreamSlices * 16;

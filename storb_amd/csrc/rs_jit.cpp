@@ -85,6 +85,23 @@ bool test_call() {
   return v;
 }
 
+// STORB_RS_JIT_STREAM=1: single calls with k > 16 run the matrix's compiled
+// kernel in its streamed form (one launch gated per slice) once it is ready.
+// Off by default: measured slower than the sliced path it replaces
+// (tools/stream_jit_ab.py, profiles/r6r_stream_jit_ab.jsonl, pageable
+// buffers, caller on the GPU's node, three interleaved pairs: (32, 48) 32 MiB
+// decode, 2 lost, 1.57-1.60 ms streamed against 0.89-1.19 ms sliced; (24, 36)
+// 6 MiB 226-245 against 196-199 us). The sliced path's compiled launches
+// start on packed slices at full width; the gated launch holds its later
+// slices' workgroups resident and polling while the host packs.
+bool stream_enabled() {
+  static const bool v = [] {
+    const char *e = std::getenv("STORB_RS_JIT_STREAM");
+    return e && *e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 size_t max_kernels() {
   static const size_t v = [] {
     const char *e = std::getenv("STORB_RS_JIT_MAX");
@@ -355,9 +372,9 @@ class Jit {
 
   static bool compile(const std::string &src, int opt, std::vector<char> &code, std::string &log) {
     hiprtcProgram prog = nullptr;
-    const char *hdrs[] = {kRsArgsH, kRsBitsliceCoreH};
-    const char *names[] = {"rs_args.h", "rs_bitslice_core.h"};
-    if (hiprtcCreateProgram(&prog, src.c_str(), "storb_bs_jit.hip", 2, hdrs, names) !=
+    const char *hdrs[] = {kRsArgsH, kRsBitsliceCoreH, kRsStreamH};
+    const char *names[] = {"rs_args.h", "rs_bitslice_core.h", "rs_stream.hpp"};
+    if (hiprtcCreateProgram(&prog, src.c_str(), "storb_bs_jit.hip", 3, hdrs, names) !=
         HIPRTC_SUCCESS)
       return false;
     const std::string o = "-O" + std::to_string(opt);
@@ -462,9 +479,9 @@ int opt_level(uint32_t k) { return k > 16 ? 1 : 3; }
 
 // Kernel symbol, so profiles tell the compiled kernels apart (bench.py and
 // profiles/summarize.py match on the "storb_bs_jit_k<k>_r<rows>_" prefix).
-std::string kernel_name(uint32_t k, uint32_t rows, uint64_t copy_mask) {
+std::string kernel_name(uint32_t k, uint32_t rows, uint64_t copy_mask, bool streamed = false) {
   return "storb_bs_jit_k" + std::to_string(k) + "_r" + std::to_string(rows) +
-         (copy_mask ? "_asm" : "_ip");
+         (copy_mask ? "_asm" : "_ip") + (streamed ? "_st" : "");
 }
 
 // Matrices of 17-32 rows run as ONE row-split launch (rs_bitslice_core.h
@@ -481,11 +498,13 @@ bool split_rows(uint32_t k, uint32_t rows) {
 // of coef[p][j] * 2^b' (the GF(2) matrix of multiplication by coef[p][j]).
 std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask,
                    int group, const bs::BsShape &sh, size_t lds, bool split,
-                   const bs::KsShape &ks) {
+                   const bs::KsShape &ks, bool streamed = false) {
   const GF256 &g = gf();
   std::string s;
   s.reserve(64 + static_cast<size_t>(rows) * k * 40);
-  s += "#include \"rs_bitslice_core.h\"\nnamespace {\nstruct JitMat {\n";
+  s += "#include \"rs_bitslice_core.h\"\n";
+  if (streamed) s += "#include \"rs_stream.hpp\"\n";
+  s += "namespace {\nstruct JitMat {\n";
   s += "  static constexpr int K = " + std::to_string(k) + ", R = " + std::to_string(rows) + ";\n";
   s += "  static constexpr unsigned long long copy_mask = " + std::to_string(copy_mask) + "ull;\n";
   s += "  struct Net { unsigned char row[R][K][8]; };\n  static constexpr Net net = {{";
@@ -516,8 +535,21 @@ std::string source(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy
   // workgroups let the allocator take 257 at k = 32 (1 wave per SIMD)
   const int threads = ks.c ? 64 * ks.c * ks.w : sh.threads;
   s += "extern \"C\" __global__ __launch_bounds__(" + std::to_string(threads) +
-       ") __attribute__((amdgpu_waves_per_eu(2))) void " + kernel_name(k, rows, copy_mask) +
-       "(const storb_rs::ApplyArgs a) {\n";
+       ") __attribute__((amdgpu_waves_per_eu(2))) void " +
+       kernel_name(k, rows, copy_mask, streamed) + "(const storb_rs::ApplyArgs a" +
+       (streamed ? ", const storb_rs::StreamArgs st" : "") + ") {\n";
+  if (streamed) {
+    // The streamed single call's gate (rs_stream.hpp): a workgroup waits for
+    // its slice's host-written ready word, runs its tile, reports the slice.
+    // One wave per tile only (the caller sizes slices in these tiles).
+    s += "  const unsigned slice = static_cast<unsigned>(blockIdx.x * " +
+         std::to_string(bs::bs_cols_per_tile(sh.threads)) + "u / st.slice_cols);\n";
+    s += "  if (!storb_rs::stream_gate(st, slice)) return;\n";
+    s += "  storb_rs::bs::bs_kernel_body<JitMat, " + std::to_string(group) + ", " +
+         std::to_string(sh.threads) + ", " + std::to_string(sh.swz) + ">(a);\n";
+    s += "  storb_rs::stream_report(st, slice);\n}\n";
+    return s;
+  }
   if (test_call()) s += "  storb_jit_test_callee(a);\n";
   if (lds >= 4 && dynamic_lds(lds) == 0) {
     // Static LDS reserving 160 KiB / cap per workgroup (occupancy cap).
@@ -565,24 +597,28 @@ bool wanted(uint32_t k, uint32_t rows, uint64_t bytes) {
 // The cache entry of a (k x r) matrix with the given copy mask: looked up,
 // or created and queued. wait: block until its compile has finished.
 static std::shared_ptr<Entry> entry_for(uint32_t k, uint32_t r, const uint8_t *coef,
-                                        uint64_t copy_mask, bool wait, bool force) {
-  const bool split = split_rows(k, r);
+                                        uint64_t copy_mask, bool wait, bool force,
+                                        bool streamed = false) {
+  // the streamed form: one wave per tile, no row split, no input split
+  const bool split = !streamed && split_rows(k, r);
   const int group = split ? bs::kSplitGroup : bs::bs_group(static_cast<int>(k), static_cast<int>(r));
-  const bs::BsShape sh = split_or_shape(k, r);
-  const bs::KsShape ks = ks_of(k, r, copy_mask);
-  const size_t lds = launch_shape(k, r, copy_mask).lds;
+  const bs::BsShape sh = streamed ? shape(k, r) : split_or_shape(k, r);
+  const bs::KsShape ks = streamed ? bs::KsShape{0, 0, 0, 0} : ks_of(k, r, copy_mask);
+  const size_t lds = streamed ? cap_lds(sh.cap, 0) : launch_shape(k, r, copy_mask).lds;
   std::string key(32 + static_cast<size_t>(r) * k, '\0');
   const uint64_t hdr[4] = {(static_cast<uint64_t>(k) << 32) | r, copy_mask,
                            (static_cast<uint64_t>(group) << 32) | lds,
                            (static_cast<uint64_t>(sh.threads) << 32) | static_cast<uint32_t>(sh.swz) |
                                (split ? 1ull << 16 : 0) |
                                (static_cast<uint64_t>(ks.c * 16 + ks.w) << 20) |
-                               (static_cast<uint64_t>(ks.g) << 26)};
+                               (static_cast<uint64_t>(ks.g) << 26) |
+                               (streamed ? 1ull << 31 : 0)};
   std::memcpy(&key[0], hdr, sizeof(hdr));
   std::memcpy(&key[32], coef, static_cast<size_t>(r) * k);
   Jit &J = jit();
-  auto e = J.get(key, kernel_name(k, r, copy_mask), opt_level(k),
-                 [&] { return source(k, r, coef, copy_mask, group, sh, lds, split, ks); }, force);
+  auto e = J.get(key, kernel_name(k, r, copy_mask, streamed), opt_level(k),
+                 [&] { return source(k, r, coef, copy_mask, group, sh, lds, split, ks, streamed); },
+                 force);
   if (e && wait) J.wait_for(*e);
   return e;
 }
@@ -673,8 +709,59 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
   return hipSuccess;
 }
 
+// The streamed form of a matrix's kernel (single calls with k > 16, whose
+// table-kernel stream measured slower than the sliced compiled kernels):
+// one wave per tile, no fused assembly, up to 8 rows -- a download's chunks
+// lose a few data shares; the one-wave 16-row k = 32 form spilled 6 VGPRs,
+// and those keep the sliced path.
+bool stream_form(uint32_t k, uint32_t rows) {
+  return stream_enabled() && k > 16 && k <= static_cast<uint32_t>(kMaxIn) && rows >= 1 &&
+         rows <= 8;
+}
+
+uint32_t stream_cols_per_tile(uint32_t k, uint32_t rows) {
+  return bs::bs_cols_per_tile(shape(k, rows).threads);
+}
+
+hipError_t try_launch_stream(int device, const ApplyArgs &a, const uint8_t *coef,
+                             const StreamArgs &st, hipStream_t s, bool *launched) {
+  *launched = false;
+  if (!stream_form(a.k, a.r) || a.ncopy || a.accumulate || a.nstripes != 1 ||
+      !wanted(a.k, a.r, static_cast<uint64_t>(a.k + a.r) * a.block) || !vector_ok(a))
+    return hipSuccess;
+  auto e = entry_for(a.k, a.r, coef, 0, false, false, true);
+  Jit &J = jit();
+  if (!e || e->state != Entry::Ready) {
+    J.fallbacks++;
+    return hipSuccess;
+  }
+  hipFunction_t f = nullptr;
+  hipError_t r = J.function(*e, device, &f);
+  if (r != hipSuccess) return r;
+  const bs::BsShape sh = shape(a.k, a.r);
+  const uint64_t cpt = bs::bs_cols_per_tile(sh.threads);
+  const uint64_t blocks = ((a.block >> 4) + cpt - 1) / cpt;
+  if (blocks == 0 || blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  ApplyArgs arg = a;
+  StreamArgs sa = st;
+  void *params[] = {&arg, &sa};
+  r = hipModuleLaunchKernel(f, static_cast<unsigned>(blocks), 1, 1,
+                            static_cast<unsigned>(sh.threads), 1, 1,
+                            static_cast<unsigned>(dynamic_lds(cap_lds(sh.cap, 0))), s, params,
+                            nullptr);
+  if (r == hipSuccess) r = J.used(*e, device, s);
+  if (r != hipSuccess) return r;
+  J.launches++;
+  *launched = true;
+  return hipSuccess;
+}
+
 int prepare(uint32_t k, uint32_t rows, const uint8_t *coef, uint64_t copy_mask, bool wait) {
   if (!enabled() || !valu_bound(k, rows)) return 0;
+  if (!copy_mask && stream_form(k, rows)) {  // the single calls' streamed form too
+    auto e = entry_for(k, rows, coef, 0, wait, true, true);
+    if (!e || e->state == Entry::Failed) return e ? -1 : 0;
+  }
   int res = 1;
   for (uint32_t b = 0; b < row_blocks(k, rows); b++) {
     const uint32_t r0 = row_start(k, rows, b), rr = row_start(k, rows, b + 1) - r0;

@@ -36,6 +36,17 @@ hipError_t try_launch(int device, const ApplyArgs &a, uint8_t *const *d_out,
                       const size_t *out_stride, const uint8_t *coef, hipStream_t s,
                       bool *launched);
 
+// The streamed single call's form of a matrix's compiled kernel (k > 16,
+// <= 8 rows; host_calls.cpp streamed): the workgroups of the one launch
+// wait per slice on host-written ready words (rs_stream.hpp). Columns per
+// workgroup tile, for sizing the slices.
+bool stream_form(uint32_t k, uint32_t rows);
+uint32_t stream_cols_per_tile(uint32_t k, uint32_t rows);
+// Launch it (a: one stripe, a.r rows, a.out set) if compiled; queue its
+// compile otherwise. *launched = false: the caller takes another path.
+hipError_t try_launch_stream(int device, const ApplyArgs &a, const uint8_t *coef,
+                             const StreamArgs &st, hipStream_t s, bool *launched);
+
 // Queue the compile of matrix `coef` (rows x k) with the given copy mask,
 // or with wait finish it. 1 = ready, -1 = failed, 0 = pending / not wanted.
 // Needs no GPU (hipRTC only).

@@ -1,9 +1,13 @@
 // rs_stream.hpp -- the device half of the streamed single calls (StreamArgs,
 // rs_args.h; host half: host_calls.cpp streamed): a workgroup waits for its
 // slice's host-written ready word, and reports its slice's completion.
+// Self-contained under hipRTC too: the run-time-compiled decode kernels'
+// streamed form (rs_jit.cpp) includes it as an in-memory header.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 
 #include "rs_args.h"
 

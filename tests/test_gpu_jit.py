@@ -306,3 +306,52 @@ print(json.dumps(dict(_lib.jit_stats(), ok=ok)))
     assert st["ok"]
     assert st["loaded"] <= 3 and st["compiled"] == 10 and st["evicted"] == 7, st
     assert st["failed"] == 0
+
+
+STREAM_CHILD = r"""
+import json, sys
+import numpy as np
+from oracle import coracle
+from storb_amd import _lib
+ctx = _lib.Context(0)
+out = []
+for k, n, B, lost in json.loads(sys.argv[1]):
+    data = np.frombuffer(np.random.default_rng(k + B).bytes(k * B), np.uint8).copy()
+    shares, b, pad = coracle.encode(k, n, data)
+    surv = [i for i in range(n) if i not in lost][:k]
+    _lib.jit_prepare_decode(k, n, surv, False, True)  # both forms compiled before the calls
+    st0 = ctx.stats()
+    ok = all(ctx.decode(k, n, [shares[i] for i in surv], surv, b, pad) == data.tobytes()
+             for _ in range(3))
+    st1 = ctx.stats()
+    out.append({"ok": ok, "streamed": st1["streamed_calls"] - st0["streamed_calls"],
+                "fallbacks": st1["stream_fallbacks"] - st0["stream_fallbacks"]})
+print(json.dumps(out))
+"""
+
+
+def test_single_call_decode_streams_compiled_kernel():
+    """Per-chunk decode with k > 16 (Storb's 16-160 GiB objects: 32 MiB chunks,
+    k = 32; piece.rs:384-386 through the shim's storb_rs_decode) with
+    STORB_RS_JIT_STREAM=1: once the matrix's compiled kernel is ready the call
+    runs its streamed form -- one launch whose workgroups wait per slice on
+    host-written words (rs_jit.cpp try_launch_stream, rs_stream.hpp). Off by
+    default (measured slower than the sliced path), so a child process with
+    the knob set. Bytes equal the oracle's; repeated calls (the per-slice
+    counters carry across calls); ragged shares; 2-8 rows; k = 24 / 32 / 64."""
+    import json
+    import os
+    import subprocess
+    import sys
+    cases = [(32, 48, 1 << 20, [0, 1]), (32, 48, 1 << 20, [4, 9, 31]),
+             (32, 48, (1 << 20) - 48, list(range(8))), (24, 36, 256 << 10, [0, 23]),
+             (64, 96, 512 << 10, [10, 11])]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", STREAM_CHILD, json.dumps(cases)], cwd=root,
+                       env=dict(os.environ, STORB_RS_JIT_STREAM="1"), capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    for case, g in zip(cases, got):
+        assert g["ok"], case
+        assert g["streamed"] == 3 and g["fallbacks"] == 0, (case, g)
