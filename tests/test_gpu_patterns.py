@@ -311,6 +311,7 @@ def test_descriptor_slots_reused_across_streams(ctx):
         assert torch.equal(out, ref), (i, plan[i])
 
 
+@pytest.mark.gpu
 def test_alternating_caller_streams_take_no_device_syncs(ctx):
     """the stream-ordering fallbacks (a table's or a descriptor
     slot's last use on a stream no order mark covers) synchronise the whole

@@ -168,8 +168,10 @@ std::vector<Var> variants() {
     v.push_back(x);
   };
   for (bool heavy : {false, true}) {
-    for (int cap : {0, 8, 10, 12, 16}) ks(std::integral_constant<int, 2>{}, cap, heavy);
-    for (int cap : {0, 8}) ks(std::integral_constant<int, 4>{}, cap, heavy);
+    for (int cap : {0, 8, 12}) ks(std::integral_constant<int, 2>{}, cap, heavy);
+    for (int cap : {0, 4, 6, 8}) ks(std::integral_constant<int, 4>{}, cap, heavy);
+    if constexpr (KM == 32)
+      for (int cap : {0, 2, 3, 4}) ks(std::integral_constant<int, 8>{}, cap, heavy);
   }
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
