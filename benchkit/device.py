@@ -207,8 +207,8 @@ def download_leg(ctx, w, stream, a, reps=100):
                    "from simulated download arrivals, one storb_rs_decode_stripes_dev per batch",
            "ms_per_call": round(ms, 4), "calls": reps, "settle": settled,
            "host_us_per_call": round(host_us, 1),
-           "kernel": (f"rs_apply_desc_mix_ks<{min(k, 32)}, 2>" if k == 16
-                      else f"rs_apply_desc_mix<{min(k, 32)}>"),
+           "kernel": ({16: "rs_apply_desc_mix_ks<16, 2>", 32: "rs_apply_desc_mix_ks<32, 4>"}.get(k)
+                      or f"rs_apply_desc_mix<{min(k, 32)}>"),
            "lost_data_shares_histogram": dict(sorted(hist.items())),
            "distinct_patterns": len({tuple(sorted(x)[:k]) for x in sets}),
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -304,7 +304,8 @@ def kernel_names(kernel, w):
                            else jit_name(w, "encode") if "encode" in w.jit_legs
                            else f"rs_apply_{table}<{min(w.k, 32)},{w.n - w.k}>")
     if "decode" in w.legs and w.sets is not None:
-        mix = "rs_apply_desc_mix_ks<16, 2>" if w.k == 16 else f"rs_apply_desc_mix<{min(w.k, 32)}>"
+        mix = ({16: "rs_apply_desc_mix_ks<16, 2>", 32: "rs_apply_desc_mix_ks<32, 4>"}.get(w.k)
+               or f"rs_apply_desc_mix<{min(w.k, 32)}>")
         names["decode"] = (f"{mix} (per-stripe descriptors: one "
                            f"launch for the stripes that lost 1-4 data shares, one per larger "
                            f"count; descriptors copied in by copy_u32x4_kernel)")

@@ -848,17 +848,23 @@ constexpr int mix_occ(int KM) { return KM <= 4 ? 16 : KM == 32 ? 3 : 0; }
 // k = 16 (config 5's download mix) runs the input-split tiles, two waves per
 // 1 KiB tile (rs_apply_desc_mix_ks<16, 2>), uncapped: tools/mixbench.hip on
 // config 5's download shape, records heaviest first as apply_desc orders
-// them, 76.0-76.7 -> 77.8-77.9 % of 8 TB/s (profiles/r6i_mixbench16.txt,
-// r6j_mixbench16.txt); four waves per tile 70-71 %. At k = 32 neither two,
-// four nor eight waves gained (72.7-74.4 against 74.7 %), so it keeps the
-// one-wave-per-256-lane shape. Fused assembly (copy) keeps rs_apply_desc_mix.
+// them, 76.0-76.9 -> 77.4-77.9 % of 8 TB/s (profiles/r6i_mixbench16.txt,
+// r6j_*, r6l_*); four waves per tile 70-77 %. k = 32 (config 6's): four waves
+// per tile (8 inputs each), 4 per CU, 72.8 -> 74.1 % against the one-tile
+// 256-lane kernel with the same heaviest-first records on one box
+// (profiles/r6t_mixbench32.txt; two waves 72.9-73.2, eight 57-63). Fused
+// assembly (copy) keeps rs_apply_desc_mix.
 template <int KM>
-constexpr int mix_ks_waves() { return KM == 16 ? 2 : 0; }
+constexpr int mix_ks_waves() { return KM == 16 ? 2 : KM == 32 ? 4 : 0; }
+template <int KM>
+constexpr int mix_ks_cap() { return KM == 32 ? 4 : 0; }
 
 template <int KM>
 hipError_t launch_desc_mix(const DescArgs &a, hipStream_t s) {
   if constexpr (mix_ks_waves<KM>() > 0)
-    if (!a.copy && a.tpw == 1) return launch_desc_mix_ks<KM, mix_ks_waves<KM>()>(a, s, a.cap);
+    if (!a.copy && a.tpw == 1)
+      return launch_desc_mix_ks<KM, mix_ks_waves<KM>()>(
+          a, s, a.cap ? static_cast<int>(a.cap) : mix_ks_cap<KM>());
   constexpr uint64_t TILE = mix_threads<KM>();
   const uint64_t tps = ((a.block >> 4) + TILE - 1) / TILE;
   if (a.tpw != 1) return hipErrorInvalidConfiguration;  // one tile per workgroup
