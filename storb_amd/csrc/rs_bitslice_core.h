@@ -34,6 +34,10 @@
 #ifndef STORB_RS_NT_STORES
 #define STORB_RS_NT_STORES 1
 #endif
+// 64-bit shifts in two of the transposition's three layers (transpose8).
+#ifndef STORB_BS_SHIFT64
+#define STORB_BS_SHIFT64 1
+#endif
 
 namespace storb_rs {
 namespace bs {
@@ -75,22 +79,56 @@ __device__ __forceinline__ void swapmove(uint32_t &lo, uint32_t &hi) {
   hi = sel(Mk, l >> S, h);
 }
 
+// Two swapmoves at once, (x[i], x[i+D]) and (x[i+1], x[i+1+D]) for even i:
+// the two lo registers and the two hi registers each shift as one 64-bit
+// value (v_lshrrev_b64 / v_lshlrev_b64 on an aligned register pair, full rate
+// on gfx950: tools/valu64_probe.hip). The bits that cross the dword boundary
+// land where the masks are zero (Mk's top S bits, (Mk << S)'s low S bits), so
+// the selects are unchanged: 6 VALU ops for two swaps instead of 8.
+template <int S, uint32_t Mk>
+__device__ __forceinline__ void swapmove2(uint32_t &lo0, uint32_t &lo1, uint32_t &hi0,
+                                          uint32_t &hi1) {
+  const uint64_t l = (static_cast<uint64_t>(lo1) << 32) | lo0;
+  const uint64_t h = (static_cast<uint64_t>(hi1) << 32) | hi0;
+  // asm: LLVM splits a 64-bit shift whose halves are used apart into
+  // v_alignbit + a 32-bit shift (and rebuilds pairs with v_mov / v_or)
+  uint64_t hs, ls;
+  asm("v_lshlrev_b64 %0, %2, %1" : "=v"(hs) : "v"(h), "n"(S));
+  asm("v_lshrrev_b64 %0, %2, %1" : "=v"(ls) : "v"(l), "n"(S));
+  const uint32_t l0 = lo0, l1 = lo1, h0 = hi0, h1 = hi1;
+  lo0 = sel(Mk << S, static_cast<uint32_t>(hs), l0);
+  lo1 = sel(Mk << S, static_cast<uint32_t>(hs >> 32), l1);
+  hi0 = sel(Mk, static_cast<uint32_t>(ls), h0);
+  hi1 = sel(Mk, static_cast<uint32_t>(ls >> 32), h1);
+}
+
 // 8 dwords (32 bytes; byte q of dword r at bit 8q..8q+7 of x[r]) <-> 8
 // bit-planes (bit b of byte q of dword r at bit 8q + r of x[b]). The three
-// layers act on disjoint index bits, so the network is its own inverse.
+// layers act on disjoint index bits, so they commute and the network is its
+// own inverse. The index-bit-2 and index-bit-1 layers pair registers that
+// sit in aligned pairs (x[0..3] / x[4..7] come from dwordx4 loads) and run as
+// swapmove2; the index-bit-0 layer pairs the two halves of one register pair
+// and stays 32-bit. 40 VALU ops per transpose (48 with 32-bit shifts only).
 __device__ __forceinline__ void transpose8(uint32_t (&x)[8]) {
-  swapmove<1, 0x55555555u>(x[0], x[1]);
-  swapmove<1, 0x55555555u>(x[2], x[3]);
-  swapmove<1, 0x55555555u>(x[4], x[5]);
-  swapmove<1, 0x55555555u>(x[6], x[7]);
-  swapmove<2, 0x33333333u>(x[0], x[2]);
-  swapmove<2, 0x33333333u>(x[1], x[3]);
-  swapmove<2, 0x33333333u>(x[4], x[6]);
-  swapmove<2, 0x33333333u>(x[5], x[7]);
+#if STORB_BS_SHIFT64
+  swapmove2<4, 0x0F0F0F0Fu>(x[0], x[1], x[4], x[5]);
+  swapmove2<4, 0x0F0F0F0Fu>(x[2], x[3], x[6], x[7]);
+  swapmove2<2, 0x33333333u>(x[0], x[1], x[2], x[3]);
+  swapmove2<2, 0x33333333u>(x[4], x[5], x[6], x[7]);
+#else
   swapmove<4, 0x0F0F0F0Fu>(x[0], x[4]);
   swapmove<4, 0x0F0F0F0Fu>(x[1], x[5]);
   swapmove<4, 0x0F0F0F0Fu>(x[2], x[6]);
   swapmove<4, 0x0F0F0F0Fu>(x[3], x[7]);
+  swapmove<2, 0x33333333u>(x[0], x[2]);
+  swapmove<2, 0x33333333u>(x[1], x[3]);
+  swapmove<2, 0x33333333u>(x[4], x[6]);
+  swapmove<2, 0x33333333u>(x[5], x[7]);
+#endif
+  swapmove<1, 0x55555555u>(x[0], x[1]);
+  swapmove<1, 0x55555555u>(x[2], x[3]);
+  swapmove<1, 0x55555555u>(x[4], x[5]);
+  swapmove<1, 0x55555555u>(x[6], x[7]);
 }
 
 __device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {

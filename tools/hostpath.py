@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import torch  # noqa: E402,F401  (HIP runtime before the library, storb_amd/_lib.py)
 
-import bench  # noqa: E402
+from benchkit import SEED_BASE, device as bdev, host as bhost  # noqa: E402
 from storb_amd import _lib  # noqa: E402
 
 
@@ -36,12 +36,12 @@ def main():
         _lib.LIB_PATH = os.path.abspath(a.lib)
     ctx = _lib.Context(0)
     erased = [0] if a.n > a.k else []
-    r = bench.host_path_rate(ctx, a.k, a.n, a.chunk, nchunks=a.chunks, reps=a.reps, erased=erased,
-                             sets=bench.download_sets(a.k, a.n, 64, bench.SEED_BASE + 4343))
+    r = bhost.host_path_rate(ctx, a.k, a.n, a.chunk, nchunks=a.chunks, reps=a.reps, erased=erased,
+                             sets=bdev.download_sets(a.k, a.n, 64, SEED_BASE + 4343))
     r.pop("what", None)
     out = {"lib": a.lib, "reps": a.reps, "k": a.k, "n": a.n, "chunk": a.chunk, "chunks": a.chunks,
            "env": {x: os.environ.get(x) for x in ("STORB_RS_ZC_BATCH", "STORB_RS_HOST_THREADS")},
-           **r, "pcie": bench.pcie_ceiling(torch.device("cuda", 0))}
+           **r, "pcie": bhost.pcie_ceiling(torch.device("cuda", 0))}
     print(json.dumps(out), flush=True)
     ctx.close()
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The per-chunk drop-in calls (bench.py shim_path_rate) for one library
+"""The per-chunk drop-in calls (benchkit/host.py shim_path_rate) for one library
 setting per process -- STORB_RS_HOST_THREADS is read at context creation:
   STORB_RS_HOST_THREADS=16 python tools/shimpath.py
   python tools/shimpath.py --lib path/to/libstorb_rs.so   (another build, for an A/B)
@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import torch  # noqa: E402,F401  (HIP runtime before the library)
 
-import bench  # noqa: E402
+from benchkit import host as bhost  # noqa: E402
 from storb_amd import _lib  # noqa: E402
 
 
@@ -21,7 +21,7 @@ def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--lib":
         _lib.LIB_PATH = os.path.abspath(sys.argv[2])
     ctx = _lib.Context(0)
-    r = bench.shim_path_rate(ctx, seconds=0.6)
+    r = bhost.shim_path_rate(ctx, seconds=0.6)
     out = {"lib": _lib.LIB_PATH, "threads": os.environ.get("STORB_RS_HOST_THREADS"),
            "rows": [{"k": g["k"], "m": g["m_total"],
                      **{x: g[x]["median_us"] for x in ("encode_call", "encode_shim", "decode_call",
