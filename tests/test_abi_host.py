@@ -300,3 +300,24 @@ def test_jit_largest_kernels_make_no_calls(tmp_path):
     for c in cos:
         r, why = _lib.code_object_calls(open(c, "rb").read())
         assert r == 0, (c, why)
+
+
+def test_marshal_chunks_arrays():
+    """The arrays decode_chunks_raw hands storb_rs_decode_chunks: one address
+    per share in chunk order, the share indices beside them, counts per chunk;
+    non-uint8 / non-contiguous shares are converted (and kept alive)."""
+    import numpy as np
+    from storb_amd import _lib
+
+    B = 64
+    base = np.arange(3 * 4 * B, dtype=np.uint8).reshape(3, 4, B)
+    odd = np.arange(2 * B, dtype=np.uint8)[::2]  # strided: copied
+    chunks = [([base[0, 1], base[0, 3]], [1, 3]), ([base[1, 0], odd, bytes(B)], [0, 2, 5]),
+              ([base[2, 2]], [4])]
+    ptrs, idx, cnt, keep = _lib.marshal_chunks(chunks, B)
+    assert ptrs.dtype == np.uint64 and idx.dtype == np.uint32 and cnt.dtype == np.uint32
+    assert cnt.tolist() == [2, 3, 1] and idx.tolist() == [1, 3, 0, 2, 5, 4]
+    assert ptrs[0] == base[0, 1].ctypes.data and ptrs[1] == base[0, 3].ctypes.data
+    assert ptrs[2] == base[1, 0].ctypes.data and ptrs[5] == base[2, 2].ctypes.data
+    assert len(keep) == 6 and keep[3].flags.c_contiguous and keep[3].ctypes.data == ptrs[3]
+    assert bytes(keep[3]) == bytes(odd) and keep[4].ctypes.data == ptrs[4]

@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import torch  # noqa: E402,F401  (HIP runtime before the library, storb_amd/_lib.py)
 
-from benchkit import SEED_BASE, device as bdev, host as bhost  # noqa: E402
+from benchkit import SEED_BASE, cpu as bcpu, device as bdev, host as bhost  # noqa: E402
 from storb_amd import _lib  # noqa: E402
 
 
@@ -34,6 +34,8 @@ def main():
     a = ap.parse_args()
     if a.lib:
         _lib.LIB_PATH = os.path.abspath(a.lib)
+    pin = bcpu.pin_rank(0)  # as bench.py: onto the GPU's NUMA node first
+    pin.pop("allowed")
     ctx = _lib.Context(0)
     erased = [0] if a.n > a.k else []
     r = bhost.host_path_rate(ctx, a.k, a.n, a.chunk, nchunks=a.chunks, reps=a.reps, erased=erased,
@@ -41,6 +43,7 @@ def main():
     r.pop("what", None)
     out = {"lib": a.lib, "reps": a.reps, "k": a.k, "n": a.n, "chunk": a.chunk, "chunks": a.chunks,
            "env": {x: os.environ.get(x) for x in ("STORB_RS_ZC_BATCH", "STORB_RS_HOST_THREADS")},
+           "pin": pin,
            **r, "pcie": bhost.pcie_ceiling(torch.device("cuda", 0))}
     print(json.dumps(out), flush=True)
     ctx.close()

@@ -4,7 +4,9 @@
 // per instruction (rs_bitslice_core.h).
 // Every variant: 16 independent dword chains per lane, ITER rounds; full
 // occupancy (8 waves per SIMD). Reported: dword-ops per second, i.e. a 64-bit
-// shift counts 2 dwords.
+// shift counts 2 dwords. Then v_bitop3_b32 at 1, 2, 4 and 8 waves per SIMD
+// with 16 independent chains and with one dependent chain per lane: the
+// issue rate a kernel gets at its own occupancy.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 valu64_probe.hip -o _build/valu64_probe
 #include <hip/hip_runtime.h>
 
@@ -65,6 +67,22 @@ __global__ __launch_bounds__(256) void k_bitop3(uint32_t *out) {
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+template <int CH>
+__global__ __launch_bounds__(256) void k_chain(uint32_t *out) {
+  uint32_t v[CH];
+#pragma unroll
+  for (int i = 0; i < CH; i++) v[i] = threadIdx.x * 16 + i;
+  for (int it = 0; it < ITER * 16 / CH; it++) {
+#pragma unroll
+    for (int i = 0; i < CH; i++)
+      asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(v[i]) : "v"(v[(i + 1) % CH]), "v"(v[(i + 2) % CH]));
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < CH; i++) s ^= v[i];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 int main() {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -90,6 +108,21 @@ int main() {
       const double inst = lanes * ITER * v.insts;
       std::printf("%-16s %8.3f ms  %7.2f T lane-inst/s  %7.2f T dword-ops/s\n", v.name, ms,
                   inst / (ms * 1e-3) / 1e12, inst * v.dwords_per_inst / (ms * 1e-3) / 1e12);
+    }
+  // occupancy sweep: w workgroups of 4 waves per CU = w waves per SIMD
+  for (int w : {1, 2, 4, 8})
+    for (int ch : {16, 1}) {
+      auto f = ch == 16 ? k_chain<16> : k_chain<1>;
+      hipLaunchKernelGGL(f, dim3(cus * w), dim3(256), 0, 0, out);
+      CK(hipEventRecord(a));
+      for (int r = 0; r < 4; r++) hipLaunchKernelGGL(f, dim3(cus * w), dim3(256), 0, 0, out);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      const double inst = (double)cus * w * 256 * 4 * ITER * 16;
+      std::printf("v_bitop3_b32 %d wave(s)/SIMD, %2d chain(s): %7.2f T lane-inst/s  %.3f wave-inst/cycle/SIMD at 2.4 GHz\n",
+                  w, ch, inst / (ms * 1e-3) / 1e12, inst / 64 / (ms * 1e-3) / (cus * 4.0) / 2.4e9);
     }
   return 0;
 }
