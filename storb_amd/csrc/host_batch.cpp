@@ -384,15 +384,26 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
     if (o < outlen)
       copy_nt(out + static_cast<size_t>(c) * out_stride + o, src, std::min(block, outlen - o));
   };
-  if (!plain.empty())  // all data shares present: concatenation (zfec does the same)
-    pool.run(static_cast<int>(plain.size()), [&](int i) {
-      for (uint32_t s = 0; s < k; s++) put_row(plain[i], s, sp(plain[i], s));
-    });
-  if (rest.empty()) return STORB_RS_OK;
+  // Chunks with all k data shares present are a concatenation (zfec does the
+  // same). Their host copies overlap the GPU work of the others: slice i of
+  // n is copied while the device runs batch i (copy_plain(i, n)).
+  auto copy_plain = [&](size_t i, size_t n) {
+    const size_t a = plain.size() * i / n, b = plain.size() * (i + 1) / n;
+    if (b > a)
+      pool.run(static_cast<int>(b - a), [&](int j) {
+        for (uint32_t s = 0; s < k; s++) put_row(plain[a + j], s, sp(plain[a + j], s));
+      });
+  };
+  if (rest.empty()) {
+    copy_plain(0, 1);
+    return STORB_RS_OK;
+  }
   DeviceGuard dg(ctx->device);
   const size_t S = round_up(block, kAlign);
-  if (!desc_ok(ctx, k, n, S))
+  if (!desc_ok(ctx, k, n, S)) {
+    copy_plain(0, 1);
     return decode_chunks_grouped(ctx, k, block, outlen, rest, pats, slot_ptr, out, out_stride);
+  }
   const size_t W = 2 * static_cast<size_t>(k) + kSlotR;
 
   // Zero-copy chunks: page-locked caller shares AND output, no padding.
@@ -443,6 +454,7 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
     pool.run(static_cast<int>(rows.size()), [&](int i) {  // overlaps the kernels
       put_row(rows[i].first, rows[i].second, sp(rows[i].first, rows[i].second));
     });
+    if (staged.empty()) copy_plain(0, 1);  // also under the kernels
     HIP_TRY(ctx, hipStreamSynchronize(ctx->pipe[0]));
   }
   if (staged.empty()) return STORB_RS_OK;
@@ -459,7 +471,17 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
     HIP_TRY(ctx, ctx->pipe_dev[b].ensure(static_cast<size_t>(k + emax) * S * batch));
   }
   const uint32_t nb = static_cast<uint32_t>((staged.size() + batch - 1) / batch);
-  // rebuilt row r of the c-th chunk of a batch: pitch emax rows per chunk
+  // Rebuilt rows of a batch packed chunk after chunk (row_off: rows before
+  // staged chunk i within its batch), so the D2H moves only the rows rebuilt
+  // -- download patterns mix chunks that lost 1 and 8 shares; an emax-row
+  // pitch copied every chunk's emax rows back.
+  std::vector<uint32_t> row_off(staged.size());
+  for (size_t i = 0; i < staged.size(); i++)
+    row_off[i] = i % batch ? row_off[i - 1] + static_cast<uint32_t>(pats[staged[i - 1]]->missing.size())
+                           : 0;
+  auto batch_rows = [&](uint32_t c0, uint32_t cn) {
+    return static_cast<size_t>(row_off[c0 + cn - 1]) + pats[staged[c0 + cn - 1]]->missing.size();
+  };
   auto unpack = [&](uint32_t bi) {
     const uint8_t *src = ctx->pipe_out[bi & 1].p;
     const uint32_t c0 = bi * batch, cn = std::min<uint32_t>(batch, static_cast<uint32_t>(staged.size()) - c0);
@@ -467,7 +489,7 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
       const uint32_t ch = staged[c0 + c];
       const Pattern &p = *pats[ch];
       for (size_t r = 0; r < p.missing.size(); r++)
-        put_row(ch, p.missing[r], src + (static_cast<size_t>(c) * emax + r) * S);
+        put_row(ch, p.missing[r], src + (static_cast<size_t>(row_off[c0 + c]) + r) * S);
     });
   };
   std::vector<const Pattern *> bp;
@@ -505,15 +527,17 @@ static int decode_chunks_locked(storb_rs_ctx *ctx, uint32_t k, uint32_t n, size_
       for (uint32_t sl = 0; sl < k; sl++)
         ptr[c * W + sl] = reinterpret_cast<uint64_t>(dd + static_cast<size_t>(c) * per + sl * S);
       for (size_t r = 0; r < p.missing.size(); r++)
-        ptr[c * W + k + r] = reinterpret_cast<uint64_t>(dm + (static_cast<size_t>(c) * emax + r) * S);
+        ptr[c * W + k + r] =
+            reinterpret_cast<uint64_t>(dm + (static_cast<size_t>(row_off[c0 + c]) + r) * S);
     }
     // staged shares are S-pitched: the kernel works on S-byte rows
     const int rc = apply_desc(ctx, k, S, false, bp, ptr, s);
     if (rc) return rc;
     HIP_TRY(ctx, st.after_k(b));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, static_cast<size_t>(emax) * S * cn,
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pipe_out[b].p, dm, batch_rows(c0, cn) * S,
                                 hipMemcpyDeviceToHost, st.out));
     HIP_TRY(ctx, st.after_out(b));
+    copy_plain(bi, nb);  // while the device runs batch bi
   }
   for (uint32_t bi = nb >= 2 ? nb - 2 : 0; bi < nb; bi++) {
     HIP_TRY(ctx, st.host_wait(bi & 1));

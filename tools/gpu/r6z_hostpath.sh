@@ -8,6 +8,8 @@ out=gpurun_out/r6z; mkdir -p $out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_patterns.py -m gpu -x -q \
   -k "chunks" --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -20 $out/tests.log; exit 1; }
 tail -1 $out/tests.log
+timeout -k 10 150 python tools/fuzz.py --seconds ${FUZZ_S:-60} --seed 6107 > $out/fuzz.json 2> $out/fuzz.err || { tail -5 $out/fuzz.err; exit 1; }
+tail -c 400 $out/fuzz.json; echo
 for g in "4 6 1048576 256" "16 24 8388608 32"; do
   set -- $g
   for z in 1 0; do
