@@ -191,6 +191,57 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  if (only && std::string(only) == "c3") {
+    // config 3's decode shape with no GF work: RS(8,4) decode of 3 rows, 8
+    // in + 3 out, 4096 contiguous stripes of 32 KiB shares, over workgroup
+    // sizes and caps (the product: rs_apply_perm<8,3> T=256 cap 4, 0.80)
+    const uint64_t B = 32u << 10, ns = 4096, bytes = ns * 11 * B;
+    const uint32_t cols = static_cast<uint32_t>(B / 16);
+    uint8_t *u;
+    CK(hipMalloc(&u, bytes));
+    CK(hipMemset(u, 0x44, bytes));
+    std::vector<Variant> vs;
+    auto add83 = [&](int T, int cap) {
+      const uint32_t blocks = static_cast<uint32_t>(ns * (cols / T));
+      vs.push_back(Variant{"config3 8+3 T=" + std::to_string(T) + " cap=" + std::to_string(cap),
+                           static_cast<double>(bytes),
+                           [=](hipStream_t st) {
+                             if (T == 256)
+                               launch<dl_uniform<8, 3, 256>>(blocks, 256, cap_lds(cap), st, u, cols);
+                             else if (T == 128)
+                               launch<dl_uniform<8, 3, 128>>(blocks, 128, cap_lds(cap), st, u, cols);
+                             else
+                               launch<dl_uniform<8, 3, 64>>(blocks, 64, cap_lds(cap), st, u, cols);
+                           },
+                           {}});
+    };
+    for (int cap : {0, 2, 3, 4, 5, 6, 8}) add83(256, cap);
+    for (int cap : {0, 6, 8, 10, 12}) add83(128, cap);
+    for (int cap : {0, 12, 16, 20, 24}) add83(64, cap);
+    for (auto &v : vs) v.run(s);
+    CK(hipStreamSynchronize(s));
+    for (int r = 0; r < rounds; r++)
+      for (auto &v : vs) {
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < reps; i++) v.run(s);
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.ms.push_back(ms / reps);
+      }
+    std::printf("c3: 4096 x (8 + 3) x 32 KiB contiguous, %.1f MB per launch, %d rounds x %d launches\n",
+                bytes / 1e6, rounds, reps);
+    for (auto &v : vs) {
+      std::sort(v.ms.begin(), v.ms.end());
+      const float med = v.ms[v.ms.size() / 2];
+      std::printf("  %-46s %8.1f us  %7.1f GB/s  frac %.3f (best %.3f)\n", v.name.c_str(),
+                  med * 1e3, v.bytes / (med * 1e-3) / 1e9, v.bytes / (med * 1e-3) / 8e12,
+                  v.bytes / (v.ms[0] * 1e-3) / 8e12);
+    }
+    CK(hipFree(u));
+    return 0;
+  }
   for (const Shape &sh : shapes) {
     if (only && std::string(only) != sh.name) continue;
     const uint64_t chunk = sh.k * sh.B;
