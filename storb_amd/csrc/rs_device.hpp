@@ -994,10 +994,32 @@ inline uint64_t tile_blocks(const ApplyArgs &a) {
   return ((cols + TILE - 1) / TILE) * a.nstripes;
 }
 
+// Launch shape of a uniform table-kernel launch without fused assembly, where
+// it differs from Tune (whose T / G the streamed and descriptor launches
+// share). <8,3> (config 3's decode of 3 lost shares; k = 5..8 encodes with
+// 3 parity rows): one-wave workgroups, load groups of 4, 16 resident per CU
+// -- 82.4 -> 83.3 % of 8 TB/s at config 3's in-place layout
+// (tools/kbench_tune.hip occ, profiles/r6s_occ_c3.txt; 64-lane caps 14-20
+// within 0.5 points, 10-12 fall to 69-78 %). The shape's no-GF ceiling:
+// 0.814 for 256-lane workgroups at 4 per CU against 0.851 for one-wave
+// workgroups at 12 (tools/dlprobe.hip c3, profiles/r6s_dlprobe_c3.txt).
+template <int KM, int RM>
+struct PermShape {
+  static constexpr int T = Tune<KM, RM>::T, G = Tune<KM, RM>::G, OCC = Tune<KM, RM>::OCC;
+};
+template <>
+struct PermShape<8, 3> {
+  static constexpr int T = 64, G = 4, OCC = 16;
+};
+
 template <int KM, int RM>
 hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
   using C = Tune<KM, RM>;
-  return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC, C::OCC_COPY);
+  using P = PermShape<KM, RM>;
+  if (a.ncopy || (P::T == C::T && P::G == C::G && P::OCC == C::OCC))
+    return launch_perm<KM, RM, C::T, C::U, C::BAR, C::G, C::TL, C::PAIR>(a, s, C::OCC,
+                                                                         C::OCC_COPY);
+  return launch_perm<KM, RM, P::T, C::U, C::BAR, P::G, C::TL, C::PAIR>(a, s, P::OCC, 0);
 }
 
 template <int KM>

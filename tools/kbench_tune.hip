@@ -168,14 +168,17 @@ int main(int argc, char **argv) {
     add_occ<8, 3>(o[1].vs);
     for (int n : {0, 8, 10, 12, 16})
       o[1].vs.push_back(mk_occ<8, 3, 128, 1, false, 8, true, true>(n));
-    for (int n : {0, 16, 20, 24, 32})
+    for (int n : {0, 10, 12, 14, 16, 20, 24, 32})
       o[1].vs.push_back(mk_occ<8, 3, 64, 1, false, 8, true, true>(n));
+    for (int n : {10, 12, 14, 16})
+      o[1].vs.push_back(mk_occ<8, 3, 64, 1, false, 4, true, true>(n));
     for (int n : {0, 3, 4, 5})
       o[1].vs.push_back(mk_occ<8, 3, 256, 1, false, 4, true, true>(n));
     add_occ<16, 8>(o[2].vs);
     add_occ<16, 2>(o[3].vs);
     add_occ<8, 4>(o[4].vs);
     ws = o;
+    if (argc > 4) ws = {o[std::atoi(argv[4])]};  // one workload of the sweep
   } else if (argc > 2) {
     ws.erase(ws.begin(), ws.begin() + std::atoi(argv[2]));
   }
