@@ -177,6 +177,10 @@ int main(int argc, char **argv) {
     add_occ<16, 8>(o[2].vs);
     add_occ<16, 2>(o[3].vs);
     add_occ<8, 4>(o[4].vs);
+    for (int n : {12, 14, 16, 20})  // one-wave workgroups (config 3's <8,3> shape)
+      o[4].vs.push_back(mk_occ<8, 4, 64, 1, false, 4, true, true>(n));
+    for (int n : {14, 16})
+      o[4].vs.push_back(mk_occ<8, 4, 64, 1, false, 8, true, true>(n));
     ws = o;
     if (argc > 4) ws = {o[std::atoi(argv[4])]};  // one workload of the sweep
   } else if (argc > 2) {
