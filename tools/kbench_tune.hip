@@ -58,6 +58,7 @@ struct W {
   std::vector<V> vs;
   bool inplace = false;  // decode layout of bench --config 3 (see below)
   int order = 0;  // survivor order: 0 index, 1 library slot order (parity in the holes), 2 parity first
+  bool copy = false;  // inplace layout, but rebuilt into a separate chunk buffer (fused assembly)
 };
 
 template <int KM, int RM, int T, int U, bool BAR, int G, bool TL = false, bool PAIR = false>
@@ -95,6 +96,29 @@ V mk_occ(int wg_per_cu) {
     return hipGetLastError();
   };
   return v;
+}
+
+// Fused-assembly (COPY) kernels under a cap: decode into a separate chunk
+// buffer, config 3's assembly leg (argv[3] = "copy").
+template <int KM, int RM, int T, bool BAR, int G, bool TL, bool PAIR>
+V mk_copy(int wg_per_cu) {
+  char buf[112];
+  std::snprintf(buf, sizeof buf, "COPY <%d,%d> T=%d G=%d TL=%d PAIR=%d wg/CU<=%d", KM, RM, T, G,
+                (int)TL, (int)PAIR, wg_per_cu);
+  const size_t stat = TL ? sizeof(PermTab) * KM * RM : 0;
+  const size_t lds = wg_per_cu ? ((160u << 10) / wg_per_cu) / 1024 * 1024 - stat : 0;
+  return V{buf, [lds](const ApplyArgs &a, hipStream_t s) {
+             auto kern = rs_apply_perm<KM, RM, T, 1, BAR, G, TL, PAIR, true>;
+             if (lds > (64u << 10)) {
+               hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  static_cast<int>(lds));
+               if (e != hipSuccess) return e;
+             }
+             const uint64_t blocks = (((a.block >> 4) + T - 1) / T) * a.nstripes;
+             hipLaunchKernelGGL(kern, dim3(blocks), dim3(T), lds, s, a);
+             return hipGetLastError();
+           }, {}};
 }
 
 template <int KM, int RM>
@@ -183,6 +207,18 @@ int main(int argc, char **argv) {
       o[4].vs.push_back(mk_occ<8, 4, 64, 1, false, 8, true, true>(n));
     ws = o;
     if (argc > 4) ws = {o[std::atoi(argv[4])]};  // one workload of the sweep
+  } else if (argc > 3 && std::strcmp(argv[3], "copy") == 0) {
+    W c{"W2c RS(8,4) decode e=3 into a separate chunk buffer (config 3 assembly)", 8, 3, 4096,
+        32 << 10, {}, true, 0, true};
+    for (int n : {0, 3, 4, 5, 6})
+      c.vs.push_back(mk_copy<8, 3, 256, false, 8, true, true>(n));
+    for (int n : {12, 14, 16, 20, 24})
+      c.vs.push_back(mk_copy<8, 3, 64, false, 4, true, true>(n));
+    for (int n : {14, 16, 20})
+      c.vs.push_back(mk_copy<8, 3, 64, false, 8, true, true>(n));
+    for (int n : {6, 8, 10})
+      c.vs.push_back(mk_copy<8, 3, 128, false, 4, true, true>(n));
+    ws = {c};
   } else if (argc > 2) {
     ws.erase(ws.begin(), ws.begin() + std::atoi(argv[2]));
   }
@@ -194,8 +230,9 @@ int main(int argc, char **argv) {
   for (auto &w : ws) {
     const uint64_t in_bytes = (uint64_t)w.n_stripes * w.k * w.B;
     const uint64_t out_bytes = (uint64_t)w.n_stripes * w.r * w.B;
-    uint8_t *in, *out;
+    uint8_t *in, *out, *dst = nullptr;
     CK(hipMalloc(&in, in_bytes));
+    if (w.copy) CK(hipMalloc(&dst, in_bytes));
     CK(hipMalloc(&out, w.inplace ? (uint64_t)w.n_stripes * 4 * w.B : out_bytes));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)in, in_bytes / 8, w.k);
     if (w.inplace)  // random "parity" too: zero inputs raise the clock (DVFS)
@@ -237,8 +274,16 @@ int main(int argc, char **argv) {
         a.in_stride[j] = surv[j] < 8 ? 8 * w.B : 4 * w.B;
       }
       for (int i = 0; i < 3; i++) {
-        a.out[i] = in + lost[i] * w.B;
+        a.out[i] = (w.copy ? dst : in) + lost[i] * w.B;
         a.out_stride[i] = 8 * w.B;
+      }
+      if (w.copy) {  // the surviving data shares stored to their slots of dst as loaded
+        for (int j = 0; j < 8; j++)
+          if (surv[j] < 8) {
+            a.copy[j] = dst + surv[j] * w.B;
+            a.copy_stride[j] = 8 * w.B;
+            a.ncopy++;
+          }
       }
     }
     a.ptab = dt;
@@ -267,7 +312,21 @@ int main(int argc, char **argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         v.us.push_back(ms * 1000.f / reps);
       }
-    const double bytes = (double)in_bytes + out_bytes;
+    // COPY: k*B read + k*B written per stripe (the bench's assembly leg)
+    const double bytes = w.copy ? 2.0 * in_bytes : (double)in_bytes + out_bytes;
+    if (w.copy) {  // every variant bit-exact against the first (the product shape)
+      std::vector<uint8_t> r0(in_bytes), r1(in_bytes);
+      for (size_t vi = 0; vi < w.vs.size(); vi++) {
+        CK(hipMemset(dst, 0, in_bytes));
+        CK(w.vs[vi].fn(a, s));
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(vi ? r1.data() : r0.data(), dst, in_bytes, hipMemcpyDeviceToHost));
+        if (vi && std::memcmp(r0.data(), r1.data(), in_bytes)) {
+          std::printf("MISMATCH %s %s\n", w.name, w.vs[vi].name.c_str());
+          return 2;
+        }
+      }
+    }
     std::printf("%s: %.3f GB algorithmic per launch\n", w.name, bytes / 1e9);
     for (auto &v : w.vs) {
       std::sort(v.us.begin(), v.us.end());
@@ -278,6 +337,7 @@ int main(int argc, char **argv) {
     CK(hipFree(in));
     CK(hipFree(out));
     CK(hipFree(dt));
+    if (dst) CK(hipFree(dst));
   }
   return 0;
 }
