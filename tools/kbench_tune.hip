@@ -183,7 +183,7 @@ int main(int argc, char **argv) {
     add_occ<4, 2>(o[0].vs);
     for (int n : {8, 9, 10, 11, 12})  // finer caps: 128-lane workgroups
       o[0].vs.push_back(mk_occ<4, 2, 128, 1, false, 4, false, false>(n));
-    for (int n : {16, 18, 20, 22, 24})  // one wave per workgroup
+    for (int n : {12, 14, 16, 18, 20, 22, 24})  // one wave per workgroup
       o[0].vs.push_back(mk_occ<4, 2, 64, 1, false, 4, false, false>(n));
     for (int n : {2, 3, 4})  // two columns per lane under a cap
       o[0].vs.push_back(mk_occ<4, 2, 256, 2, false, 4, false, false>(n));
