@@ -1011,6 +1011,25 @@ template <>
 struct PermShape<8, 3> {
   static constexpr int T = 64, G = 4, OCC = 16;
 };
+// <4,2>: the headline RS(4,2) encode and decode of 2 lost shares, one-wave
+// workgroups at 14 per CU. The default bench line, interleaved A/B of
+// library builds on two boxes (tools/build_variant.sh, tools/gpu/r6s_ab42.sh,
+// profiles/r6s_ab42_round1/2.jsonl): 4,136-4,160 -> 4,201-4,224 GiB/s
+// (+1.5 %), config 4 4,120-4,126 -> 4,244-4,247 (+3 %). The cap is sharp:
+// 13 per CU +0.7 %, 16 (which 15 also resolves to: 10 KiB each) -1 %, 12 or
+// 22 -1.7 %; 128-lane workgroups at 7 or 8 per CU -0.5 / +0.7 %. Round 5's
+// one-wave A/B (profiles/r5m_ab_headline_t64.txt) had tried caps 12 and 16.
+// STORB_PERM42_T / _OCC: experiment builds only.
+#ifndef STORB_PERM42_T
+#define STORB_PERM42_T 64
+#endif
+#ifndef STORB_PERM42_OCC
+#define STORB_PERM42_OCC 14
+#endif
+template <>
+struct PermShape<4, 2> {
+  static constexpr int T = STORB_PERM42_T, G = 4, OCC = STORB_PERM42_OCC;
+};
 
 template <int KM, int RM>
 hipError_t go_perm(const ApplyArgs &a, hipStream_t s) {
