@@ -842,8 +842,14 @@ hipError_t launch_desc(const DescArgs &a, hipStream_t s, int occ = 0, int occ_co
 // k <= 4 keeps the RS(4,2) table kernel's measured cap of 4.
 // k = 32 (16 shares per group): 3 per CU, +0.5-0.7 % over uncapped in three
 // interleaved runs (profiles/r4{b,c,d}_mixbench32.txt "G16 cap3").
-// k <= 4 with one-wave workgroups (mix_threads): 16 per CU.
-constexpr int mix_occ(int KM) { return KM <= 4 ? 16 : KM == 32 ? 3 : 0; }
+// k <= 4 with one-wave workgroups (mix_threads): 16 per CU -- unlike the
+// uniform <4,2> launch (PermShape, 14 per CU), lower caps lose here: config 2
+// download step 0.377 ms at 16 against 0.379 / 0.386 / 0.392 at 14 / 13 / 12
+// (tools/gpu/r6s_abmix.sh, profiles/r6s_abmix.jsonl).
+#ifndef STORB_MIX4_OCC  // experiment builds only
+#define STORB_MIX4_OCC 16
+#endif
+constexpr int mix_occ(int KM) { return KM <= 4 ? STORB_MIX4_OCC : KM == 32 ? 3 : 0; }
 
 // k = 16 (config 5's download mix) runs the input-split tiles, two waves per
 // 1 KiB tile (rs_apply_desc_mix_ks<16, 2>), uncapped: tools/mixbench.hip on
