@@ -187,6 +187,15 @@ int main(int argc, char **argv) {
       o[0].vs.push_back(mk_occ<4, 2, 64, 1, false, 4, false, false>(n));
     for (int n : {2, 3, 4})  // two columns per lane under a cap
       o[0].vs.push_back(mk_occ<4, 2, 256, 2, false, 4, false, false>(n));
+    // round 6: around the one-wave product shape (PermShape<4,2>: T 64, G 4, 14 per CU)
+    for (int n : {13, 14})
+      o[0].vs.push_back(mk_occ<4, 2, 64, 1, false, 2, false, false>(n));
+    for (int n : {13, 14})
+      o[0].vs.push_back(mk_occ<4, 2, 64, 1, false, 4, false, true>(n));
+    for (int n : {13, 14})
+      o[0].vs.push_back(mk_occ<4, 2, 64, 1, true, 4, false, false>(n));
+    for (int n : {6, 7, 8})
+      o[0].vs.push_back(mk_occ<4, 2, 64, 2, false, 4, false, false>(n));
     for (int n : {2, 3})
       o[0].vs.push_back(mk_occ<4, 2, 512, 1, false, 4, false, false>(n));
     add_occ<8, 3>(o[1].vs);
