@@ -167,12 +167,12 @@ std::vector<Var> variants() {
     x.heavy_first = heavy;
     v.push_back(x);
   };
-  for (bool heavy : {false, true}) {
-    for (int cap : {0, 8, 12}) ks(std::integral_constant<int, 2>{}, cap, heavy);
-    for (int cap : {0, 4, 6, 8}) ks(std::integral_constant<int, 4>{}, cap, heavy);
-    if constexpr (KM == 32)
-      for (int cap : {0, 2, 3, 4}) ks(std::integral_constant<int, 8>{}, cap, heavy);
-  }
+  // round 6: the caps around 14 waves per CU (the table kernel's best, rs_device.hpp
+  // PermShape), records heaviest first as apply_desc orders them
+  for (int cap : {0, 5, 6, 7, 8, 10}) ks(std::integral_constant<int, 2>{}, cap, true);
+  for (int cap : {0, 3, 4, 5}) ks(std::integral_constant<int, 4>{}, cap, true);
+  if constexpr (KM == 32)
+    for (int cap : {2, 3}) ks(std::integral_constant<int, 8>{}, cap, true);
   constexpr int GP = Tune<KM, 1>::G;  // the product's group size
   v.push_back(mk<KM, GP, true, false, false>("same shape here (TL, rec[0])", 0));
   if constexpr (KM == 16) {
