@@ -1017,6 +1017,13 @@ template <>
 struct PermShape<8, 3> {
   static constexpr int T = 64, G = 4, OCC = 16;
 };
+// Not taken: <2,1> (Storb's (2, 3) encode) and <4,1> (single-row rebuilds at
+// k = 3-4) stream faster one-wave in tools/kbench_tune.hip's compact layouts
+// (<2,1> uncapped 82.9 -> 84.9 %, <4,1> at 14 per CU 81.8 -> 86.6 %;
+// profiles/r6s_occ_21*.txt, r6s_occ_41.txt), but on the product's in-place
+// repair of a data share <4,1> lost 10 % (0.2014 -> 0.2215 ms; a parity
+// share +1 %; tools/gpu/r6s_ab41.sh, profiles/r6s_ab41.jsonl), and the
+// in-place decodes of <2,1> are unmeasured -- so both keep Tune's shape.
 // <4,2>: the headline RS(4,2) encode and decode of 2 lost shares, one-wave
 // workgroups at 14 per CU. The default bench line, interleaved A/B of
 // library builds on two boxes (tools/build_variant.sh, tools/gpu/r6s_ab42.sh,

@@ -214,6 +214,21 @@ int main(int argc, char **argv) {
       o[4].vs.push_back(mk_occ<8, 4, 64, 1, false, 4, true, true>(n));
     for (int n : {14, 16})
       o[4].vs.push_back(mk_occ<8, 4, 64, 1, false, 8, true, true>(n));
+    // round 6: Storb's (2, 3) encode (256 KiB chunks) and single-row rebuilds at k = 4
+    o.push_back({"W7 RS(2,1) encode 4096 x 256 KiB (Storb's (2, 3))", 2, 1, 4096, 128 << 10, {}});
+    o.push_back({"W8 RS(4,1) one row from 4, 1024 x 1 MiB", 4, 1, 1024, 256 << 10, {}});
+    o[5].vs.push_back(product<2, 1>());
+    o[6].vs.push_back(product<4, 1>());
+    for (int n : {0, 4, 6, 8})
+      o[5].vs.push_back(mk_occ<2, 1, 256, 1, false, 2, false, false>(n));
+    for (int n : {12, 13, 14, 16, 20, 24, 28, 32, 0})
+      o[5].vs.push_back(mk_occ<2, 1, 64, 1, false, 2, false, false>(n));
+    for (int n : {12, 14, 16, 0})
+      o[5].vs.push_back(mk_occ<2, 1, 128, 1, false, 2, false, false>(n));
+    for (int n : {0, 4, 6})
+      o[6].vs.push_back(mk_occ<4, 1, 256, 1, false, 4, false, false>(n));
+    for (int n : {12, 13, 14, 16, 20, 24})
+      o[6].vs.push_back(mk_occ<4, 1, 64, 1, false, 4, false, false>(n));
     ws = o;
     if (argc > 4) ws = {o[std::atoi(argv[4])]};  // one workload of the sweep
   } else if (argc > 3 && std::strcmp(argv[3], "copy") == 0) {
