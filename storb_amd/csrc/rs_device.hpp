@@ -1017,13 +1017,21 @@ template <>
 struct PermShape<8, 3> {
   static constexpr int T = 64, G = 4, OCC = 16;
 };
-// Not taken: <2,1> (Storb's (2, 3) encode) and <4,1> (single-row rebuilds at
-// k = 3-4) stream faster one-wave in tools/kbench_tune.hip's compact layouts
-// (<2,1> uncapped 82.9 -> 84.9 %, <4,1> at 14 per CU 81.8 -> 86.6 %;
-// profiles/r6s_occ_21*.txt, r6s_occ_41.txt), but on the product's in-place
-// repair of a data share <4,1> lost 10 % (0.2014 -> 0.2215 ms; a parity
-// share +1 %; tools/gpu/r6s_ab41.sh, profiles/r6s_ab41.jsonl), and the
-// in-place decodes of <2,1> are unmeasured -- so both keep Tune's shape.
+// Not taken: <4,1> (single-row rebuilds at k = 3-4) streams faster one-wave
+// in tools/kbench_tune.hip's compact layout (at 14 per CU 81.8 -> 86.6 %,
+// profiles/r6s_occ_41.txt), but on the product's in-place repair of a data
+// share it lost 10 % (0.2014 -> 0.2215 ms; a parity share +1 %;
+// tools/gpu/r6s_ab41.sh, profiles/r6s_ab41.jsonl), so it keeps Tune's shape.
+// <2,1> (Storb's (2, 3) geometry, 256 KiB chunks): one-wave workgroups,
+// uncapped -- on the device batch calls (tools/ab21.py, tools/gpu/r6s_ab21.sh,
+// profiles/r6s_ab21.jsonl, builds interleaved) encode 245.6 -> 240.9 us and
+// the in-place decode of a data share 246.8 -> 240.5 us per 4096 chunks
+// (0.82 -> 0.84 of 8 TB/s); kbench W7: 28-32 per CU the same, 24 and below
+// lose (profiles/r6s_occ_21*.txt).
+template <>
+struct PermShape<2, 1> {
+  static constexpr int T = 64, G = 2, OCC = 0;
+};
 // <4,2>: the headline RS(4,2) encode and decode of 2 lost shares, one-wave
 // workgroups at 14 per CU. The default bench line, interleaved A/B of
 // library builds on two boxes (tools/build_variant.sh, tools/gpu/r6s_ab42.sh,
