@@ -1032,6 +1032,19 @@ template <>
 struct PermShape<2, 1> {
   static constexpr int T = 64, G = 2, OCC = 0;
 };
+// <8,1> / <8,2> (Storb's (8, 12) geometry, 2 MiB chunks: 1-2 data shares
+// rebuilt in place): one-wave workgroups, load groups of 4, 16 per CU --
+// 196.8 -> 187.5 us and 216.6 -> 212.4 us per 1024 x 1 MiB of shares
+// (tools/ab21.py AB_K=8, tools/gpu/r6s_ab8r.sh, profiles/r6s_ab8r.jsonl,
+// builds interleaved; 14 per CU the same for one row, noisy for two).
+template <>
+struct PermShape<8, 1> {
+  static constexpr int T = 64, G = 4, OCC = 16;
+};
+template <>
+struct PermShape<8, 2> {
+  static constexpr int T = 64, G = 4, OCC = 16;
+};
 // <4,2>: the headline RS(4,2) encode and decode of 2 lost shares, one-wave
 // workgroups at 14 per CU. The default bench line, interleaved A/B of
 // library builds on two boxes (tools/build_variant.sh, tools/gpu/r6s_ab42.sh,
